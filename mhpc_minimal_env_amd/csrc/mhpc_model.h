@@ -1,0 +1,383 @@
+// Hand-written planar-quadruped physics for the MHPC solve path.
+//
+// Replaces, as device code, every CasADi-generated kernel the reference calls on its
+// HSDDP path:
+//   Dyn_FL / Dyn_BS / Dyn_FS      -> wb_dynamics()          (PlanarQuadruped.cpp:8-27)
+//   Dyn_*_par                     -> wb_dynamics<Dual>()    (PlanarQuadruped.cpp:30-53)
+//   Imp_F / Imp_B (+ _par)        -> wb_impact()            (PlanarQuadruped.cpp:58-100)
+//   WB_FL1/FL2_terminal_constr    -> wb_touchdown()         (MHPCConstraints.cpp:91-107)
+//   Jacob_F / Jacob_B             -> wb_foot_jacobian()     (PlanarQuadruped.cpp:103-117)
+//   FBDynamics / FBDynamics_par   -> srb_dynamics(), srb_jacobians() (PlanarFloatingBase.cpp:7-72)
+//
+// Model: q = (x, z, theta, q_fhip, q_fknee, q_bhip, q_bknee),
+// x = (q, qdot), u = torques on the four leg joints.  A point a distance l "down" a link
+// whose absolute angle is a sits at (-l sin a, -l cos a) from that link's joint; the
+// front/back hips sit at (x +- 0.19 cos th, z -+ 0.19 sin th).  M(q) and the bias
+// h(q, qdot) are assembled body by body from CoM Jacobians (M = sum m Jc'Jc + Ic w w',
+// h = sum m Jc'(Jcdot qdot + g)), which is exact for a planar tree.  Stance and impact
+// solve the contact KKT system through the Schur complement J M^-1 J' of a Cholesky
+// factor of M (the reference's generated code uses an unpivoted QR instead; both agree
+// to ~1e-12, see tests/test_model_host.py).
+//
+// Everything is templated on the scalar so the same source runs in double (rollouts)
+// and in Dual (one Jacobian column per lane).
+#pragma once
+#include "mhpc_dual.h"
+
+namespace mhpc {
+
+// ---- parameters baked into the reference's generated code ----------
+constexpr double kGrav = 9.81;
+constexpr double kBodyMass = 5.46;
+constexpr double kBodyInertia = 0.116419;        // about the body CoM
+constexpr double kHipX = 0.19;                   // hip joints at +-0.19 on the body axis
+constexpr double kThighMass = 1.268;
+constexpr double kThighCom = 0.02;               // CoM distance down the thigh
+constexpr double kThighInertiaJoint = 0.0047132; // about the hip joint
+constexpr double kThighLen = 0.209;              // hip -> knee
+constexpr double kShankMass = 0.128;
+constexpr double kShankCom = 0.061;
+constexpr double kShankInertiaJoint = 0.000972288;  // about the knee joint
+constexpr double kShankLen = 0.195;              // knee -> foot
+constexpr double kGroundHeight = -0.404;         // MHPCLocomotion.cpp:25, WB_FL*_terminal_constr.c
+constexpr double kThighInertiaCom = kThighInertiaJoint - kThighMass * kThighCom * kThighCom;
+constexpr double kShankInertiaCom = kShankInertiaJoint - kShankMass * kShankCom * kShankCom;
+
+// SRB constants (FBDynamics.c:51-100): total mass and pitch inertia of the floating base.
+constexpr double kSrbMass = 8.2520000000000007;
+constexpr double kSrbInertia = 0.23216549759999999;
+constexpr double kSrbInvInertia = 4.3072722275163766;  // as folded by FBDynamics_par.c
+constexpr double kSrbInvMass = 1.2118274357731458e-01;
+
+constexpr int kWbX = 14, kWbQ = 7, kWbU = 4, kWbY = 4;
+constexpr int kFbX = 6, kFbU = 4, kFbY = 4;
+
+enum Foot { kFront = 0, kBack = 1 };
+
+// Geometry of one leg: absolute link angles and their sines/cosines.
+template <class S>
+struct LegGeo {
+  S s1, c1, s2, c2;  // thigh angle a1 = th + q_hip, shank angle a2 = a1 + q_knee
+  S w1, w2;          // absolute angular rates
+};
+
+template <class S>
+struct WbGeo {
+  S sth, cth;        // body pitch
+  LegGeo<S> leg[2];  // [front, back]
+};
+
+template <class S>
+MHPC_HD void wb_geometry(const S* x, WbGeo<S>& g) {
+  sin_cos(x[2], &g.sth, &g.cth);
+  for (int f = 0; f < 2; ++f) {
+    const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+    const S a1 = x[2] + x[ih];
+    const S a2 = a1 + x[ik];
+    sin_cos(a1, &g.leg[f].s1, &g.leg[f].c1);
+    sin_cos(a2, &g.leg[f].s2, &g.leg[f].c2);
+    g.leg[f].w1 = x[9] + x[7 + ih];
+    g.leg[f].w2 = g.leg[f].w1 + x[7 + ik];
+  }
+}
+
+// Jacobian of a point on leg f at distance l1 down the thigh and l2 down the shank,
+// compact over the local columns (x, z, th, hip, knee); plus Jdot*qdot.
+template <class S>
+MHPC_HD void leg_point_jac(const WbGeo<S>& g, int f, double l1, double l2,
+                           S jx[5], S jz[5], S* jdx, S* jdz) {
+  const double sg = f == kFront ? 1.0 : -1.0;
+  const LegGeo<S>& L = g.leg[f];
+  // d/da of l*(-sin a, -cos a) = l*(-cos a, sin a)
+  const S tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
+  const S tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
+  jx[0] = S(1.0); jz[0] = S(0.0);
+  jx[1] = S(0.0); jz[1] = S(1.0);
+  jx[4] = tx2;    jz[4] = tz2;
+  jx[3] = tx1 + tx2;
+  jz[3] = tz1 + tz2;
+  jx[2] = (-sg * kHipX) * g.sth + jx[3];
+  jz[2] = (-sg * kHipX) * g.cth + jz[3];
+  // centripetal terms of the two link offsets (the hip offset is added by the caller)
+  *jdx = L.w1 * L.w1 * (l1 * L.s1) + L.w2 * L.w2 * (l2 * L.s2);
+  *jdz = L.w1 * L.w1 * (l1 * L.c1) + L.w2 * L.w2 * (l2 * L.c2);
+}
+
+// M(q) (full symmetric 7x7) and bias h(q, qdot) = C qdot + g.
+template <class S>
+MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[7][7], S h[7]) {
+  for (int i = 0; i < 7; ++i) {
+    h[i] = S(0.0);
+    for (int j = 0; j < 7; ++j) M[i][j] = S(0.0);
+  }
+  const S thd2 = x[9] * x[9];
+  M[0][0] = S(kBodyMass);
+  M[1][1] = S(kBodyMass);
+  M[2][2] = S(kBodyInertia);
+  h[1] = S(kBodyMass * kGrav);
+  for (int f = 0; f < 2; ++f) {
+    const double sg = f == kFront ? 1.0 : -1.0;
+    const int idx[5] = {0, 1, 2, 3 + 2 * f, 4 + 2 * f};
+    // centripetal acceleration of the hip point
+    const S hax = (-sg * kHipX) * g.cth * thd2;
+    const S haz = (sg * kHipX) * g.sth * thd2;
+    for (int b = 0; b < 2; ++b) {  // thigh, shank
+      S jx[5], jz[5], jdx, jdz;
+      double m, ic;
+      int nc;
+      if (b == 0) {
+        leg_point_jac(g, f, kThighCom, 0.0, jx, jz, &jdx, &jdz);
+        m = kThighMass; ic = kThighInertiaCom; nc = 4;
+      } else {
+        leg_point_jac(g, f, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
+        m = kShankMass; ic = kShankInertiaCom; nc = 5;
+      }
+      jdx += hax;
+      jdz += haz;
+      const S ax = jdx, az = jdz + kGrav;
+      for (int a = 0; a < nc; ++a) {
+        h[idx[a]] += m * (jx[a] * ax + jz[a] * az);
+        for (int c = 0; c <= a; ++c) {
+          S v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
+          if (a >= 2 && c >= 2) v += ic;
+          M[idx[a]][idx[c]] += v;
+        }
+      }
+    }
+  }
+  for (int i = 0; i < 7; ++i)
+    for (int j = i + 1; j < 7; ++j) M[i][j] = M[j][i];
+}
+
+// In-place Cholesky M = L L' (lower triangle holds L).
+template <class S>
+MHPC_HD void chol7(S A[7][7]) {
+  for (int j = 0; j < 7; ++j) {
+    S d = A[j][j];
+    for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
+    const S l = sqrt_(d);
+    A[j][j] = l;
+    for (int i = j + 1; i < 7; ++i) {
+      S s = A[i][j];
+      for (int k = 0; k < j; ++k) s -= A[i][k] * A[j][k];
+      A[i][j] = s / l;
+    }
+  }
+}
+
+template <class S>
+MHPC_HD void chol7_solve(const S L[7][7], S b[7]) {
+  for (int i = 0; i < 7; ++i) {
+    S s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i][k] * b[k];
+    b[i] = s / L[i][i];
+  }
+  for (int i = 6; i >= 0; --i) {
+    S s = b[i];
+    for (int k = i + 1; k < 7; ++k) s -= L[k][i] * b[k];
+    b[i] = s / L[i][i];
+  }
+}
+
+// Foot Jacobian (2x7, dense) and Jdot*qdot of foot f.
+template <class S>
+MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, int f, S J[2][7], S jd[2]) {
+  S jx[5], jz[5], jdx, jdz;
+  leg_point_jac(g, f, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
+  const double sg = f == kFront ? 1.0 : -1.0;
+  const S thd2 = x[9] * x[9];
+  jd[0] = jdx + (-sg * kHipX) * g.cth * thd2;
+  jd[1] = jdz + (sg * kHipX) * g.sth * thd2;
+  for (int i = 0; i < 7; ++i) { J[0][i] = S(0.0); J[1][i] = S(0.0); }
+  const int idx[5] = {0, 1, 2, 3 + 2 * f, 4 + 2 * f};
+  for (int a = 0; a < 5; ++a) { J[0][idx[a]] = jx[a]; J[1][idx[a]] = jz[a]; }
+}
+
+// Schur-complement solve of the contact KKT system
+//   [M -J'; J 0] [v; lam] = [rhs; -c]  ->  v = M^-1 (rhs + J' lam)
+// given the Cholesky factor L of M.
+template <class S>
+MHPC_HD void kkt_contact(const S L[7][7], const S J[2][7], const S c[2], S v[7], S lam[2]) {
+  // v currently holds M^-1 rhs
+  S Y[2][7];
+  for (int r = 0; r < 2; ++r) {
+    for (int i = 0; i < 7; ++i) Y[r][i] = J[r][i];
+    chol7_solve(L, Y[r]);
+  }
+  S A00 = S(0.0), A01 = S(0.0), A11 = S(0.0), r0 = -c[0], r1 = -c[1];
+  for (int i = 0; i < 7; ++i) {
+    A00 += J[0][i] * Y[0][i];
+    A01 += J[0][i] * Y[1][i];
+    A11 += J[1][i] * Y[1][i];
+    r0 -= J[0][i] * v[i];
+    r1 -= J[1][i] * v[i];
+  }
+  const S det = A00 * A11 - A01 * A01;
+  lam[0] = (A11 * r0 - A01 * r1) / det;
+  lam[1] = (A00 * r1 - A01 * r0) / det;
+  for (int i = 0; i < 7; ++i) v[i] += Y[0][i] * lam[0] + Y[1][i] * lam[1];
+}
+
+// Continuous whole-body dynamics: xdot = (qdot, qddot), y = contact force of the stance
+// foot in its slots (front -> y[0:2], back -> y[2:4]); zero in flight.
+// mode 1: back stance (Dyn_BS), 2/4: flight (Dyn_FL), 3: front stance (Dyn_FS).
+template <class S>
+MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
+  WbGeo<S> g;
+  wb_geometry(x, g);
+  S M[7][7], h[7];
+  wb_mass_bias(x, g, M, h);
+  chol7(M);
+  S v[7];
+  v[0] = -h[0]; v[1] = -h[1]; v[2] = -h[2];
+  for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
+  chol7_solve(M, v);
+  for (int i = 0; i < 4; ++i) y[i] = S(0.0);
+  if (mode == 1 || mode == 3) {
+    const int f = mode == 3 ? kFront : kBack;
+    S J[2][7], jd[2], lam[2];
+    wb_foot_jac_full(x, g, f, J, jd);
+    kkt_contact(M, J, jd, v, lam);
+    y[2 * f] = lam[0];
+    y[2 * f + 1] = lam[1];
+  }
+  for (int i = 0; i < 7; ++i) {
+    xdot[i] = x[7 + i];
+    xdot[7 + i] = v[i];
+  }
+}
+
+// Plastic impact of foot f (Imp_F: f = front, end of mode 2; Imp_B: back, end of mode 4):
+// q+ = q, [M -J'; J 0][qd+; Lam] = [M qd-; 0].
+template <class S>
+MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
+  WbGeo<S> g;
+  wb_geometry(x, g);
+  S M[7][7], h[7];
+  wb_mass_bias(x, g, M, h);
+  chol7(M);
+  S J[2][7], jd[2];
+  wb_foot_jac_full(x, g, f, J, jd);
+  S v[7], c[2];
+  for (int i = 0; i < 7; ++i) v[i] = x[7 + i];   // M^-1 (M qd-) = qd-
+  c[0] = S(0.0); c[1] = S(0.0);
+  // J qd+ = 0  <=>  J v + J Y lam = 0 with rhs -c = 0
+  kkt_contact(M, J, c, v, Lam);
+  for (int i = 0; i < 7; ++i) {
+    xp[i] = x[i];
+    xp[7 + i] = v[i];
+  }
+}
+
+// Touchdown constraint h = foot_z + 0.404 with its gradient and Hessian (dense, 14x14
+// row-major); foot f = front for mode 2 (WB_FL1), back for mode 4 (WB_FL2).
+MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double* hxx) {
+  const double sg = f == kFront ? 1.0 : -1.0;
+  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+  double sth, cth, s1, c1, s2, c2;
+  sin_cos(x[2], &sth, &cth);
+  const double a1 = x[2] + x[ih];
+  const double a2 = a1 + x[ik];
+  sin_cos(a1, &s1, &c1);
+  sin_cos(a2, &s2, &c2);
+  *h = x[1] - sg * kHipX * sth - kThighLen * c1 - kShankLen * c2 - kGroundHeight;
+  for (int i = 0; i < 14; ++i) hx[i] = 0.0;
+  for (int i = 0; i < 196; ++i) hxx[i] = 0.0;
+  const double dk = kShankLen * s2;
+  const double dh = kThighLen * s1 + dk;
+  hx[1] = 1.0;
+  hx[2] = -sg * kHipX * cth + dh;
+  hx[ih] = dh;
+  hx[ik] = dk;
+  const double ek = kShankLen * c2;
+  const double eh = kThighLen * c1 + ek;
+  const double et = sg * kHipX * sth + eh;
+  const int id[3] = {2, ih, ik};
+  const double Hs[3][3] = {{et, eh, ek}, {eh, eh, ek}, {ek, ek, ek}};
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) hxx[id[a] * 14 + id[b]] = Hs[a][b];
+}
+
+// Foot Jacobian J (2x7, row-major) and Jdot (2x7) as used by the PD warm start
+// (Jacob_F / Jacob_B; boundingPDControl.cpp:29,35).
+MHPC_HD void wb_foot_jacobian(const double* x, int f, double* J, double* Jd) {
+  WbGeo<double> g;
+  wb_geometry(x, g);
+  double Jm[2][7], jd[2];
+  wb_foot_jac_full(x, g, f, Jm, jd);
+  for (int r = 0; r < 2; ++r)
+    for (int i = 0; i < 7; ++i) J[r * 7 + i] = Jm[r][i];
+  // Jdot = d/dt J: columns th, hip, knee carry the rates of the link directions.
+  const double sg = f == kFront ? 1.0 : -1.0;
+  const LegGeo<double>& L = g.leg[f];
+  const double thd = x[9];
+  for (int i = 0; i < 14; ++i) Jd[i] = 0.0;
+  // d/dt of -l*cos a = l sin a * adot ; d/dt of l*sin a = l cos a * adot
+  const double kx = kShankLen * L.s2 * L.w2, kz = kShankLen * L.c2 * L.w2;
+  const double hx = kThighLen * L.s1 * L.w1 + kx, hz = kThighLen * L.c1 * L.w1 + kz;
+  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+  Jd[0 * 7 + ik] = kx;  Jd[1 * 7 + ik] = kz;
+  Jd[0 * 7 + ih] = hx;  Jd[1 * 7 + ih] = hz;
+  Jd[0 * 7 + 2] = -sg * kHipX * g.cth * thd + hx;
+  Jd[1 * 7 + 2] = sg * kHipX * g.sth * thd + hz;
+}
+
+// Hip-to-foot vector of leg f (PlanarQuadruped::get_leg_ext_vec, PlanarQuadruped.cpp:195-205).
+MHPC_HD void wb_leg_ext(const double* q, int f, double* v) {
+  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+  double s1, c1, s2, c2;
+  sin_cos(q[2] + q[ih], &s1, &c1);
+  sin_cos(q[2] + q[ih] + q[ik], &s2, &c2);
+  v[0] = -kThighLen * s1 - kShankLen * s2;
+  v[1] = -kThighLen * c1 - kShankLen * c2;
+}
+
+// Hip x position of leg f for the SRB foothold planner (FootholdPlan.h:26-50 via
+// PlanarQuadruped::get_contact_position with the hip link frame).
+MHPC_HD double wb_hip_x(const double* pos3, int f) {
+  const double sg = f == kFront ? 1.0 : -1.0;
+  return pos3[0] + sg * kHipX * cos(pos3[2]);
+}
+
+// ---- single rigid body (PlanarFloatingBase + FBDynamics) ---------------------------
+// x = (px, pz, th, vx, vz, w), u = (FFx, FFz, FBx, FBz), p = footholds (pFx, pFz, pBx,
+// pBz), s = contact flags (front, back).  Operation order follows FBDynamics.c so the
+// SRB arithmetic is bit-identical to the reference's.
+MHPC_HD void srb_contact(int mode, double s[2]) {
+  s[0] = mode == 3 ? 1.0 : 0.0;
+  s[1] = mode == 1 ? 1.0 : 0.0;
+}
+
+MHPC_HD void srb_dynamics(const double* x, const double* u, const double* p, const double* s,
+                          double* xd) {
+  xd[0] = x[3];
+  xd[1] = x[4];
+  xd[2] = x[5];
+  xd[3] = (s[0] * u[0]) / kSrbMass + (s[1] * u[2]) / kSrbMass;
+  xd[4] = ((s[0] * u[1]) / kSrbMass + (s[1] * u[3]) / kSrbMass) + (-9.8100000000000005);
+  const double tf = ((p[1] - x[1]) * u[0] - (p[0] - x[0]) * u[1]) / kSrbInertia;
+  const double tb = ((p[3] - x[1]) * u[2] - (p[2] - x[0]) * u[3]) / kSrbInertia;
+  xd[5] = s[0] * tf + s[1] * tb;
+}
+
+// Continuous Jacobians, dense row-major Ac (6x6) and Bc (6x4) (FBDynamics_par.c).
+MHPC_HD void srb_jacobians(const double* x, const double* u, const double* p, const double* s,
+                           double* Ac, double* Bc) {
+  for (int i = 0; i < 36; ++i) Ac[i] = 0.0;
+  for (int i = 0; i < 24; ++i) Bc[i] = 0.0;
+  Ac[5 * 6 + 0] = s[0] * (kSrbInvInertia * u[1]) + s[1] * (kSrbInvInertia * u[3]);
+  Ac[5 * 6 + 1] = -(s[0] * (kSrbInvInertia * u[0]) + s[1] * (kSrbInvInertia * u[2]));
+  Ac[0 * 6 + 3] = 1.0;
+  Ac[1 * 6 + 4] = 1.0;
+  Ac[2 * 6 + 5] = 1.0;
+  Bc[3 * 4 + 0] = kSrbInvMass * s[0];
+  Bc[5 * 4 + 0] = s[0] * (kSrbInvInertia * (p[1] - x[1]));
+  Bc[4 * 4 + 1] = kSrbInvMass * s[0];
+  Bc[5 * 4 + 1] = -(s[0] * (kSrbInvInertia * (p[0] - x[0])));
+  Bc[3 * 4 + 2] = kSrbInvMass * s[1];
+  Bc[5 * 4 + 2] = s[1] * (kSrbInvInertia * (p[3] - x[1]));
+  Bc[4 * 4 + 3] = kSrbInvMass * s[1];
+  Bc[5 * 4 + 3] = -(s[1] * (kSrbInvInertia * (p[2] - x[0])));
+}
+
+}  // namespace mhpc
