@@ -1,0 +1,149 @@
+/* mhpc_capi.h -- C-ABI boundary of the MI355X-native HSDDP solve path.
+ *
+ * Drop-in for the solve path that the reference runs under
+ * MHPCLocomotion<double>::solve_mhpc() (Controller/MHPCLocomotion/MHPCLocomotion.cpp:167-195
+ * -> HSDDPSolver/source/MultiPhaseDDP.cpp:154-289).  Plain C types only: pointers, sizes,
+ * POD structs; no exceptions cross the ABI; every entry point returns an mhpc_status
+ * (0 = OK).  One handle owns the device-resident state of a BATCH of independent MPC
+ * problems that share one phase layout (gait schedule).  Calls on one handle are
+ * serialised by the caller; different handles (devices, streams) are independent.
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   mhpc_create          MHPCLocomotion ctor + memory_alloc      (MHPCLocomotion.cpp:8-43,218-261)
+ *   mhpc_set_x0          MultiPhaseDDP::set_initial_condition   (MultiPhaseDDP.h:24-25); the
+ *                        reference overwrites _x0 with its private default in
+ *                        initialization() (MHPCLocomotion.cpp:49) -- settable here so a batch can
+ *                        carry random initial states
+ *   mhpc_initialize      MHPCLocomotion::initialization         (MHPCLocomotion.cpp:47-53):
+ *                        memory_reset + build_problem (ReferenceGen::generate_ref,
+ *                        ReferenceGen.h:53-109) + warmstart (bounding_PDcontrol,
+ *                        boundingPDControl.cpp:3-46)
+ *   mhpc_solve           MHPCLocomotion::solve_mhpc / MultiPhaseDDP::solve
+ *                        (MHPCLocomotion.cpp:167-195, MultiPhaseDDP.cpp:154-289)
+ *   mhpc_get_phase       SinglePhase::get_nominal_ms_ptr / get_CTG_info_ptr
+ *                        (SinglePhase.cpp:364-373; fields of ModelState / CostToGoStruct,
+ *                        MHPC_CompoundTypes.h:7-22,88-145)
+ *   mhpc_get_scalars     MultiPhaseDDP::_actual_cost / _exp_cost_change /
+ *                        _tconstr_violation and SinglePhaseAbstract::_V/_dV
+ *                        (MultiPhaseDDP.h:57-60, SinglePhaseAbstract.h:116-118)
+ *   mhpc_destroy         MHPCLocomotion::~MHPCLocomotion / memory_free (MHPCLocomotion.cpp:383-470)
+ */
+#ifndef MHPC_CAPI_H
+#define MHPC_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHPC_MAX_PHASES 16
+#define MHPC_MAX_KNOTS 1024
+#define MHPC_TRACE_LEN 64
+
+typedef enum {
+  MHPC_OK = 0,
+  MHPC_ERR_INVALID = 1,  /* bad argument / descriptor */
+  MHPC_ERR_DEVICE = 2,   /* HIP runtime error (message via mhpc_last_error) */
+  MHPC_ERR_STATE = 3     /* call order violated (e.g. solve before initialize) */
+} mhpc_status;
+
+/* Per-problem solve outcome (status array of mhpc_solve). */
+typedef enum {
+  MHPC_SOLVE_OK = 0,          /* finished all AL iterations or met AL_thresh */
+  MHPC_SOLVE_REG_ABORT = 1,   /* regularization > 1000: early return (MultiPhaseDDP.cpp:218-226) */
+  MHPC_SOLVE_NONFINITE = 2    /* non-finite total cost at the end of the solve */
+} mhpc_solve_status;
+
+/* Phase layout. As in MHPCLocomotion::build_problem (MHPCLocomotion.cpp:63-104) the n_wb
+ * whole-body phases come first, then n_fb single-rigid-body phases; mode_seq[p] in 1..4
+ * (1 back stance, 2 flight, 3 front stance, 4 flight); N[p] knots per phase.  dt values
+ * are the reference's float parameters promoted to double.
+ * n_wb == 0 is accepted (SRB-only problems, config C1). */
+typedef struct {
+  int32_t n_wb;
+  int32_t n_fb;
+  int32_t mode_seq[MHPC_MAX_PHASES];
+  int32_t N[MHPC_MAX_PHASES];
+  double dt_wb;
+  double dt_fb;
+  double vel_cmd;     /* USRCMD::vel (float promoted) */
+  double height_cmd;  /* USRCMD::height */
+  int32_t precision;  /* 64 (fp32 is a later extension; 32 is rejected for now) */
+  int32_t reserved;
+} mhpc_problem_desc;
+
+/* Field-for-field HSDDP_OPTION<double> (MHPC_CompoundTypes.h:196-212). */
+typedef struct {
+  double alpha;
+  double gamma;
+  double update_penalty;
+  double update_relax;
+  double update_regularization;
+  double update_ReB;
+  double max_DDP_iter;
+  double max_AL_iter;
+  double DDP_thresh;
+  double AL_thresh;
+  int32_t AL_active;
+  int32_t ReB_active;
+  int32_t smooth_active;
+  int32_t reserved;
+} mhpc_hsddp_option;
+
+/* Aggregate counters of the last mhpc_solve (sums over the batch). */
+typedef struct {
+  int64_t ddp_iters;        /* inner DDP iterations executed */
+  int64_t bws_sweeps;       /* backward sweeps incl. failed (retried) ones */
+  int64_t bws_knots;        /* knots swept backward (incl. partial failed sweeps) */
+  int64_t ls_rollouts;      /* line-search rollouts the serial reference would run */
+  int64_t fwd_sweeps;       /* full forward sweeps (forward_sweep(0)) */
+  int64_t partial_sweeps;   /* forward_sweep_partials_only calls */
+  double solve_ms;          /* device time of the last solve (HIP events) */
+} mhpc_counters;
+
+typedef struct mhpc_handle mhpc_handle;
+
+/* Library identification / diagnostics. */
+const char* mhpc_version(void);
+const char* mhpc_last_error(void);
+
+/* Number of knots/entries helpers for sizing caller buffers. */
+int mhpc_phase_dims(const mhpc_problem_desc* desc, int phase, int* xsize, int* N);
+
+int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int batch,
+                int device, mhpc_handle** out);
+/* x0: [batch][xsize of phase 0] row-major host array. */
+int mhpc_set_x0(mhpc_handle* h, const double* x0);
+int mhpc_initialize(mhpc_handle* h);
+/* status: optional host array [batch] of mhpc_solve_status. */
+int mhpc_solve(mhpc_handle* h, int32_t* status);
+/* Copy out the nominal solution of one phase; any pointer may be NULL.
+ * Shapes (row-major, host): x [batch][N][xsize], u/y/du [batch][N][4],
+ * K [batch][N][4][xsize], Vx [batch][N][xsize]. */
+int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, double* K,
+                   double* du, double* Vx);
+/* J, dV_exp, viol: [batch]; V_phase, dV_phase: [batch][n_phases]; trace: [batch][MHPC_TRACE_LEN]
+ * (decision trace, encoding in DESIGN.md §Parity); any pointer may be NULL. */
+int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
+                     double* dV_phase, int32_t* trace);
+int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
+void mhpc_destroy(mhpc_handle* h);
+
+/* ---- batched model evaluation on the device (kernel-level parity hooks) -----------
+ * Replace the CasADi C ABI of SURVEY.md table 2b for whole batches of points.  All
+ * arrays are host, row-major, n points.  Dense outputs: Ac/Px [n][14][14], Bc [n][14][4],
+ * C [n][4][14], D [n][4][4]; SRB Ac [n][6][6], Bc [n][6][4]. */
+int mhpc_eval_wb_dynamics(int device, int n, int mode, const double* x, const double* u,
+                          double* xdot, double* y);
+int mhpc_eval_wb_partials(int device, int n, int mode, const double* x, const double* u,
+                          double* Ac, double* Bc, double* C, double* D);
+int mhpc_eval_wb_impact(int device, int n, int foot, const double* x, double* xplus,
+                        double* Px);
+int mhpc_eval_srb(int device, int n, const double* x, const double* u, const double* foothold,
+                  const double* contact, double* xdot, double* Ac, double* Bc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHPC_CAPI_H */

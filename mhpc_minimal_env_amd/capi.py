@@ -1,0 +1,154 @@
+"""ctypes mirror of include/mhpc_capi.h and the loader of the native library.
+
+The product library is `mhpc_minimal_env_amd/libmhpc_amd.so` (HIP kernels for gfx950 +
+the C-ABI host runtime), built in-tree by `__graft_entry__.build()`.  There is no
+fallback: if the library is missing, `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmhpc_amd.so")
+
+MHPC_MAX_PHASES = 16
+MHPC_MAX_KNOTS = 1024
+MHPC_TRACE_LEN = 64
+
+MHPC_OK = 0
+MHPC_SOLVE_OK = 0
+MHPC_SOLVE_REG_ABORT = 1
+MHPC_SOLVE_NONFINITE = 2
+
+
+class ProblemDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_wb", ctypes.c_int32),
+        ("n_fb", ctypes.c_int32),
+        ("mode_seq", ctypes.c_int32 * MHPC_MAX_PHASES),
+        ("N", ctypes.c_int32 * MHPC_MAX_PHASES),
+        ("dt_wb", ctypes.c_double),
+        ("dt_fb", ctypes.c_double),
+        ("vel_cmd", ctypes.c_double),
+        ("height_cmd", ctypes.c_double),
+        ("precision", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+    @property
+    def n_phases(self) -> int:
+        return self.n_wb + self.n_fb
+
+    def xsize(self, p: int) -> int:
+        return 14 if p < self.n_wb else 6
+
+    def knots(self, p: int) -> int:
+        return self.N[p]
+
+    def lens(self):
+        """Per-problem phase-concatenated lengths of (x, u, K) arrays."""
+        lx = sum(self.N[p] * self.xsize(p) for p in range(self.n_phases))
+        lu = sum(self.N[p] * 4 for p in range(self.n_phases))
+        lk = sum(self.N[p] * 4 * self.xsize(p) for p in range(self.n_phases))
+        return lx, lu, lk
+
+    def describe(self) -> dict:
+        return {
+            "n_wb": self.n_wb, "n_fb": self.n_fb,
+            "mode_seq": [self.mode_seq[p] for p in range(self.n_phases)],
+            "N": [self.N[p] for p in range(self.n_phases)],
+            "dt_wb": self.dt_wb, "dt_fb": self.dt_fb,
+            "vel_cmd": self.vel_cmd, "height_cmd": self.height_cmd,
+        }
+
+
+class HsddpOption(ctypes.Structure):
+    _fields_ = [
+        ("alpha", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("update_penalty", ctypes.c_double),
+        ("update_relax", ctypes.c_double),
+        ("update_regularization", ctypes.c_double),
+        ("update_ReB", ctypes.c_double),
+        ("max_DDP_iter", ctypes.c_double),
+        ("max_AL_iter", ctypes.c_double),
+        ("DDP_thresh", ctypes.c_double),
+        ("AL_thresh", ctypes.c_double),
+        ("AL_active", ctypes.c_int32),
+        ("ReB_active", ctypes.c_int32),
+        ("smooth_active", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [
+        ("ddp_iters", ctypes.c_int64),
+        ("bws_sweeps", ctypes.c_int64),
+        ("bws_knots", ctypes.c_int64),
+        ("ls_rollouts", ctypes.c_int64),
+        ("fwd_sweeps", ctypes.c_int64),
+        ("partial_sweeps", ctypes.c_int64),
+        ("solve_ms", ctypes.c_double),
+    ]
+
+
+_DP = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int32)
+
+# (name, restype, argtypes) -- every entry point declared in include/mhpc_capi.h
+SIGNATURES = [
+    ("mhpc_version", ctypes.c_char_p, []),
+    ("mhpc_last_error", ctypes.c_char_p, []),
+    ("mhpc_phase_dims", ctypes.c_int, [ctypes.POINTER(ProblemDesc), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("mhpc_create", ctypes.c_int, [ctypes.POINTER(ProblemDesc), ctypes.POINTER(HsddpOption),
+                                   ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mhpc_set_x0", ctypes.c_int, [ctypes.c_void_p, _DP]),
+    ("mhpc_initialize", ctypes.c_int, [ctypes.c_void_p]),
+    ("mhpc_solve", ctypes.c_int, [ctypes.c_void_p, _IP]),
+    ("mhpc_get_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP]),
+    ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
+    ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
+    ("mhpc_destroy", None, [ctypes.c_void_p]),
+    ("mhpc_eval_wb_dynamics", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
+                                             _DP, _DP]),
+    ("mhpc_eval_wb_partials", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
+                                             _DP, _DP, _DP, _DP]),
+    ("mhpc_eval_wb_impact", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP, _DP]),
+    ("mhpc_eval_srb", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP, _DP]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libmhpc_amd.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build the HIP extension with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != MHPC_OK:
+        msg = lib().mhpc_last_error()
+        raise RuntimeError(f"{what} failed with status {rc}: {msg.decode() if msg else ''}")
+
+
+def dptr(a):
+    return None if a is None else a.ctypes.data_as(_DP)
+
+
+def iptr(a):
+    return None if a is None else a.ctypes.data_as(_IP)

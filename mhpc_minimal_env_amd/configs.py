@@ -1,0 +1,42 @@
+"""The BASELINE.json workloads as problem descriptors (mapping: SURVEY.md App. C).
+
+C1  1 SRB phase (mode 1), dt_fb = (float)0.0016, N = 50   -- MultiPhaseDDP(1) + SinglePhase<6,4,4>
+C2  1 WB phase (mode 1), dt_wb = (float)(0.08f/120), N = 120
+C3  2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(GaitType2D::PRONK) = default branch,
+    uniform 0.08 s, dt = (float)0.001 -> N = 80 each; "trot" in BASELINE.json
+C4  = C3, sharded over GPUs
+C5  Gait() BOUND, 4 WB + 6 SRB (fp32 in BASELINE.json; fp64 here until the fp32 path lands)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import locomotion as L
+
+
+def c1_desc():
+    d = L.make_problem_desc(0, 1, [1], [0.08], 0.001, 0.0016, 1.5)
+    assert d.N[0] == 50, d.N[0]
+    return d
+
+
+def c2_desc():
+    dt = float(np.float32(np.float32(0.08) / np.float32(120)))
+    return L.make_problem_desc(1, 0, [1], [0.08], dt, 0.001, 1.5, N=[120])
+
+
+def c3_desc():
+    params = L.MHPCUserParameters(n_wbphase=2, n_fbphase=2, usrcmd=L.USRCMD(vel=1.5))
+    return L.desc_from_params(params, L.Gait(L.GaitType2D.PRONK))
+
+
+def c5_desc():
+    params = L.MHPCUserParameters(n_wbphase=4, n_fbphase=6, usrcmd=L.USRCMD(vel=1.5))
+    return L.desc_from_params(params, L.Gait())
+
+
+def x0_for(desc, batch: int, offset: int = 0):
+    x0 = L.random_x0(batch, offset=offset)
+    if desc.n_wb == 0:
+        x0 = x0[:, L.STATE_PROJ_ROWS]
+    return np.ascontiguousarray(x0)

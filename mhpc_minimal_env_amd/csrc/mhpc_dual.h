@@ -14,6 +14,13 @@
 #define MHPC_HD inline
 #endif
 
+// Unfused multiply-add inside a block: the SRB kernels keep FBDynamics.c's rounding exactly.
+#if defined(__clang__)
+#define MHPC_NO_FMA _Pragma("clang fp contract(off)")
+#else
+#define MHPC_NO_FMA
+#endif
+
 namespace mhpc {
 
 struct Dual {

@@ -103,17 +103,18 @@ MHPC_HD void leg_point_jac(const WbGeo<S>& g, int f, double l1, double l2,
   *jdz = L.w1 * L.w1 * (l1 * L.c1) + L.w2 * L.w2 * (l2 * L.c2);
 }
 
-// M(q) (full symmetric 7x7) and bias h(q, qdot) = C qdot + g.
+// Packed lower-triangular index of the symmetric 7x7 mass matrix.
+MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// M(q) (packed lower triangle, 28 entries) and bias h(q, qdot) = C qdot + g.
 template <class S>
-MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[7][7], S h[7]) {
-  for (int i = 0; i < 7; ++i) {
-    h[i] = S(0.0);
-    for (int j = 0; j < 7; ++j) M[i][j] = S(0.0);
-  }
+MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
+  for (int i = 0; i < 7; ++i) h[i] = S(0.0);
+  for (int i = 0; i < 28; ++i) M[i] = S(0.0);
   const S thd2 = x[9] * x[9];
-  M[0][0] = S(kBodyMass);
-  M[1][1] = S(kBodyMass);
-  M[2][2] = S(kBodyInertia);
+  M[tri(0, 0)] = S(kBodyMass);
+  M[tri(1, 1)] = S(kBodyMass);
+  M[tri(2, 2)] = S(kBodyInertia);
   h[1] = S(kBodyMass * kGrav);
   for (int f = 0; f < 2; ++f) {
     const double sg = f == kFront ? 1.0 : -1.0;
@@ -138,44 +139,47 @@ MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[7][7], S h[7]) {
       for (int a = 0; a < nc; ++a) {
         h[idx[a]] += m * (jx[a] * ax + jz[a] * az);
         for (int c = 0; c <= a; ++c) {
+          // x/z columns of a CoM Jacobian are unit vectors: skip the exact zeros
+          if (a < 2 && c < 2) {
+            if (a == c) M[tri(idx[a], idx[c])] += S(m);
+            continue;
+          }
           S v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
           if (a >= 2 && c >= 2) v += ic;
-          M[idx[a]][idx[c]] += v;
+          M[tri(idx[a], idx[c])] += v;
         }
       }
     }
   }
-  for (int i = 0; i < 7; ++i)
-    for (int j = i + 1; j < 7; ++j) M[i][j] = M[j][i];
 }
 
-// In-place Cholesky M = L L' (lower triangle holds L).
+// In-place Cholesky M = L L' on the packed lower triangle.
 template <class S>
-MHPC_HD void chol7(S A[7][7]) {
+MHPC_HD void chol7(S A[28]) {
   for (int j = 0; j < 7; ++j) {
-    S d = A[j][j];
-    for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
+    S d = A[tri(j, j)];
+    for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
     const S l = sqrt_(d);
-    A[j][j] = l;
+    A[tri(j, j)] = l;
     for (int i = j + 1; i < 7; ++i) {
-      S s = A[i][j];
-      for (int k = 0; k < j; ++k) s -= A[i][k] * A[j][k];
-      A[i][j] = s / l;
+      S s = A[tri(i, j)];
+      for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
+      A[tri(i, j)] = s / l;
     }
   }
 }
 
 template <class S>
-MHPC_HD void chol7_solve(const S L[7][7], S b[7]) {
+MHPC_HD void chol7_solve(const S L[28], S b[7]) {
   for (int i = 0; i < 7; ++i) {
     S s = b[i];
-    for (int k = 0; k < i; ++k) s -= L[i][k] * b[k];
-    b[i] = s / L[i][i];
+    for (int k = 0; k < i; ++k) s -= L[tri(i, k)] * b[k];
+    b[i] = s / L[tri(i, i)];
   }
   for (int i = 6; i >= 0; --i) {
     S s = b[i];
-    for (int k = i + 1; k < 7; ++k) s -= L[k][i] * b[k];
-    b[i] = s / L[i][i];
+    for (int k = i + 1; k < 7; ++k) s -= L[tri(k, i)] * b[k];
+    b[i] = s / L[tri(i, i)];
   }
 }
 
@@ -197,7 +201,7 @@ MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, int f, S J[2][7], S
 //   [M -J'; J 0] [v; lam] = [rhs; -c]  ->  v = M^-1 (rhs + J' lam)
 // given the Cholesky factor L of M.
 template <class S>
-MHPC_HD void kkt_contact(const S L[7][7], const S J[2][7], const S c[2], S v[7], S lam[2]) {
+MHPC_HD void kkt_contact(const S L[28], const S J[2][7], const S c[2], S v[7], S lam[2]) {
   // v currently holds M^-1 rhs
   S Y[2][7];
   for (int r = 0; r < 2; ++r) {
@@ -225,7 +229,7 @@ template <class S>
 MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
   WbGeo<S> g;
   wb_geometry(x, g);
-  S M[7][7], h[7];
+  S M[28], h[7];
   wb_mass_bias(x, g, M, h);
   chol7(M);
   S v[7];
@@ -253,7 +257,7 @@ template <class S>
 MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
   WbGeo<S> g;
   wb_geometry(x, g);
-  S M[7][7], h[7];
+  S M[28], h[7];
   wb_mass_bias(x, g, M, h);
   chol7(M);
   S J[2][7], jd[2];
@@ -269,9 +273,19 @@ MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
   }
 }
 
-// Touchdown constraint h = foot_z + 0.404 with its gradient and Hessian (dense, 14x14
-// row-major); foot f = front for mode 2 (WB_FL1), back for mode 4 (WB_FL2).
-MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double* hxx) {
+// Touchdown constraint h = foot_z + 0.404 (foot f = front for mode 2 / WB_FL1, back for
+// mode 4 / WB_FL2) with its gradient hx (14) and the 3x3 non-zero block of its Hessian on
+// the state indices id[] = (theta, hip, knee) of that leg.
+MHPC_HD double wb_touchdown_value(const double* x, int f) {
+  const double sg = f == kFront ? 1.0 : -1.0;
+  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+  const double a1 = x[2] + x[ih];
+  const double a2 = a1 + x[ik];
+  return x[1] - sg * kHipX * sin(x[2]) - kThighLen * cos(a1) - kShankLen * cos(a2) - kGroundHeight;
+}
+
+MHPC_HD void wb_touchdown_compact(const double* x, int f, double* h, double* hx, int id[3],
+                                  double Hs[3][3]) {
   const double sg = f == kFront ? 1.0 : -1.0;
   const int ih = 3 + 2 * f, ik = 4 + 2 * f;
   double sth, cth, s1, c1, s2, c2;
@@ -282,7 +296,6 @@ MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double*
   sin_cos(a2, &s2, &c2);
   *h = x[1] - sg * kHipX * sth - kThighLen * c1 - kShankLen * c2 - kGroundHeight;
   for (int i = 0; i < 14; ++i) hx[i] = 0.0;
-  for (int i = 0; i < 196; ++i) hxx[i] = 0.0;
   const double dk = kShankLen * s2;
   const double dh = kThighLen * s1 + dk;
   hx[1] = 1.0;
@@ -292,8 +305,18 @@ MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double*
   const double ek = kShankLen * c2;
   const double eh = kThighLen * c1 + ek;
   const double et = sg * kHipX * sth + eh;
-  const int id[3] = {2, ih, ik};
-  const double Hs[3][3] = {{et, eh, ek}, {eh, eh, ek}, {ek, ek, ek}};
+  id[0] = 2; id[1] = ih; id[2] = ik;
+  Hs[0][0] = et; Hs[0][1] = eh; Hs[0][2] = ek;
+  Hs[1][0] = eh; Hs[1][1] = eh; Hs[1][2] = ek;
+  Hs[2][0] = ek; Hs[2][1] = ek; Hs[2][2] = ek;
+}
+
+// Dense form (row-major 14x14 Hessian), used by the host checks.
+MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double* hxx) {
+  int id[3];
+  double Hs[3][3];
+  wb_touchdown_compact(x, f, h, hx, id, Hs);
+  for (int i = 0; i < 196; ++i) hxx[i] = 0.0;
   for (int a = 0; a < 3; ++a)
     for (int b = 0; b < 3; ++b) hxx[id[a] * 14 + id[b]] = Hs[a][b];
 }
@@ -350,6 +373,7 @@ MHPC_HD void srb_contact(int mode, double s[2]) {
 
 MHPC_HD void srb_dynamics(const double* x, const double* u, const double* p, const double* s,
                           double* xd) {
+  MHPC_NO_FMA
   xd[0] = x[3];
   xd[1] = x[4];
   xd[2] = x[5];
@@ -363,6 +387,7 @@ MHPC_HD void srb_dynamics(const double* x, const double* u, const double* p, con
 // Continuous Jacobians, dense row-major Ac (6x6) and Bc (6x4) (FBDynamics_par.c).
 MHPC_HD void srb_jacobians(const double* x, const double* u, const double* p, const double* s,
                            double* Ac, double* Bc) {
+  MHPC_NO_FMA
   for (int i = 0; i < 36; ++i) Ac[i] = 0.0;
   for (int i = 0; i < 24; ++i) Bc[i] = 0.0;
   Ac[5 * 6 + 0] = s[0] * (kSrbInvInertia * u[1]) + s[1] * (kSrbInvInertia * u[3]);

@@ -1,0 +1,456 @@
+// Host runtime behind include/mhpc_capi.h: handle lifetime, HBM allocation, and the
+// fixed kernel schedule of one batched solve (MultiPhaseDDP::solve restated as launches
+// over a device-resident per-problem state machine).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mhpc_capi.h"
+#include "mhpc_solver.h"
+
+namespace mhpc {
+hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
+hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
+hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
+hipError_t launch_export(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_eval_wb_dyn(int, int, const double*, const double*, double*, double*, hipStream_t);
+hipError_t launch_eval_wb_par(int, int, const double*, const double*, double*, double*, double*,
+                              double*, hipStream_t);
+hipError_t launch_eval_wb_impact(int, int, const double*, double*, double*, hipStream_t);
+hipError_t launch_eval_srb(int, const double*, const double*, const double*, const double*,
+                           double*, double*, double*, hipStream_t);
+}  // namespace mhpc
+
+using namespace mhpc;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(MHPC_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+}  // namespace
+
+struct mhpc_handle {
+  mhpc_problem_desc desc;
+  mhpc_hsddp_option opt;
+  int device = 0;
+  SolveParams sp;
+  DevBufs d;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool x0_set = false, initialized = false, solved = false;
+  float solve_ms = 0;
+};
+
+extern "C" const char* mhpc_version(void) { return "mhpc_minimal_env_amd 0.1 (gfx950, fp64)"; }
+extern "C" const char* mhpc_last_error(void) { return g_err.c_str(); }
+
+static int validate(const mhpc_problem_desc* d) {
+  if (!d) return fail(MHPC_ERR_INVALID, "null descriptor");
+  const int P = d->n_wb + d->n_fb;
+  if (d->n_wb < 0 || d->n_fb < 0 || P < 1 || P > MHPC_MAX_PHASES)
+    return fail(MHPC_ERR_INVALID, "phase count out of range");
+  if (d->precision != 64) return fail(MHPC_ERR_INVALID, "only precision 64 is implemented");
+  int NK = 0;
+  for (int p = 0; p < P; ++p) {
+    if (d->mode_seq[p] < 1 || d->mode_seq[p] > 4) return fail(MHPC_ERR_INVALID, "mode out of range");
+    if (d->N[p] < 2) return fail(MHPC_ERR_INVALID, "each phase needs N >= 2");
+    NK += d->N[p];
+  }
+  if (NK > MHPC_MAX_KNOTS) return fail(MHPC_ERR_INVALID, "too many knots");
+  if (!(d->dt_wb > 0) || !(d->dt_fb > 0)) return fail(MHPC_ERR_INVALID, "dt must be positive");
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_phase_dims(const mhpc_problem_desc* desc, int phase, int* xsize, int* N) {
+  int rc = validate(desc);
+  if (rc) return rc;
+  if (phase < 0 || phase >= desc->n_wb + desc->n_fb) return fail(MHPC_ERR_INVALID, "bad phase");
+  if (xsize) *xsize = phase < desc->n_wb ? 14 : 6;
+  if (N) *N = desc->N[phase];
+  return MHPC_OK;
+}
+
+static void free_bufs(mhpc_handle* h) {
+  DevBufs& d = h->d;
+  void* ptrs[] = {d.traj, d.refpos, d.K, d.du, d.G, d.par, d.px, d.x0, d.st, d.out};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  memset(&d, 0, sizeof d);
+}
+
+extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int batch,
+                           int device, mhpc_handle** out) {
+  if (!out || !opt) return fail(MHPC_ERR_INVALID, "null argument");
+  *out = nullptr;
+  int rc = validate(desc);
+  if (rc) return rc;
+  if (batch < 1) return fail(MHPC_ERR_INVALID, "batch must be >= 1");
+  if (!(opt->alpha > 0 && opt->alpha < 1)) return fail(MHPC_ERR_INVALID, "alpha must be in (0,1)");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MHPC_ERR_INVALID, "no such device");
+  HIPCHK(hipSetDevice(device));
+
+  mhpc_handle* h = new mhpc_handle();
+  h->desc = *desc;
+  h->opt = *opt;
+  h->device = device;
+  SolveParams& sp = h->sp;
+  memset(&sp, 0, sizeof sp);
+  sp.B = batch;
+  sp.P = desc->n_wb + desc->n_fb;
+  sp.n_wb = desc->n_wb;
+  int ko = 0, items = 0;
+  for (int p = 0; p < sp.P; ++p) {
+    const bool wb = p < desc->n_wb;
+    sp.mode[p] = desc->mode_seq[p];
+    sp.N[p] = desc->N[p];
+    sp.ko[p] = ko;
+    sp.xs[p] = wb ? 14 : 6;
+    sp.dt[p] = wb ? desc->dt_wb : desc->dt_fb;
+    ko += desc->N[p];
+    sp.par_item_off[p] = items;
+    if (wb) items += (desc->N[p] - 1) * 18 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
+  }
+  sp.par_item_off[sp.P] = items;
+  for (int p = sp.P + 1; p <= MAXP; ++p) sp.par_item_off[p] = items;
+  sp.par_items = items;
+  sp.NK = ko;
+  sp.vel = desc->vel_cmd;
+  sp.height = desc->height_cmd;
+  // line-search grid exactly as MultiPhaseDDP::forward_iteration generates it (:130-151)
+  int nc = 0;
+  for (double eps = 1; eps > pow(0.1, 10); eps *= opt->alpha) {
+    if (nc == MAXC) {
+      delete h;
+      return fail(MHPC_ERR_INVALID, "line search needs more than 32 trials (alpha too large)");
+    }
+    sp.eps[nc++] = eps;
+  }
+  sp.n_cand = nc;
+  sp.nslot = nc + 1;
+  sp.gamma = opt->gamma;
+  sp.DDP_thresh = opt->DDP_thresh;
+  sp.AL_thresh = opt->AL_thresh;
+  sp.update_penalty = opt->update_penalty;
+  sp.update_relax = opt->update_relax;
+  sp.update_regularization = opt->update_regularization;
+  sp.update_ReB = opt->update_ReB;
+  sp.eps9 = pow(0.1, 9);
+  sp.AL_active = opt->AL_active ? 1 : 0;
+  sp.ReB_active = opt->ReB_active ? 1 : 0;
+
+  DevBufs& d = h->d;
+  memset(&d, 0, sizeof d);
+  const size_t B = batch, NK = sp.NK;
+  hipError_t e = hipSuccess;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+  };
+  alloc((void**)&d.traj, B * sp.nslot * NK * KS * sizeof(double));
+  alloc((void**)&d.refpos, B * NK * sizeof(double));
+  alloc((void**)&d.K, B * NK * 56 * sizeof(double));
+  alloc((void**)&d.du, B * NK * 4 * sizeof(double));
+  alloc((void**)&d.G, B * NK * 14 * sizeof(double));
+  alloc((void**)&d.par, B * NK * PS * sizeof(double));
+  alloc((void**)&d.px, B * MAXP * 196 * sizeof(double));
+  alloc((void**)&d.x0, B * 14 * sizeof(double));
+  alloc((void**)&d.st, B * sizeof(ProbState));
+  alloc((void**)&d.out, B * NK * KS * sizeof(double));
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&h->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+  if (e == hipSuccess) e = hipMemset(d.x0, 0, B * 14 * sizeof(double));
+  if (e != hipSuccess) {
+    free_bufs(h);
+    delete h;
+    return fail(MHPC_ERR_DEVICE, std::string("allocation failed: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_set_x0(mhpc_handle* h, const double* x0) {
+  if (!h || !x0) return fail(MHPC_ERR_INVALID, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  const int n0 = h->sp.n_wb > 0 ? 14 : 6;
+  std::vector<double> pad((size_t)h->sp.B * 14, 0.0);
+  for (int b = 0; b < h->sp.B; ++b)
+    for (int i = 0; i < n0; ++i) pad[(size_t)b * 14 + i] = x0[(size_t)b * n0 + i];
+  HIPCHK(hipMemcpyAsync(h->d.x0, pad.data(), pad.size() * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->x0_set = true;
+  h->initialized = false;
+  return MHPC_OK;
+}
+
+// initialization(): memory_reset + build_problem (refs) + warmstart, all on the device.
+static int initialize_async(mhpc_handle* h) {
+  const SolveParams& sp = h->sp;
+  DevBufs& d = h->d;
+  const size_t B = sp.B, NK = sp.NK;
+  HIPCHK(hipMemsetAsync(d.traj, 0, B * sp.nslot * NK * KS * sizeof(double), h->stream));
+  HIPCHK(hipMemsetAsync(d.K, 0, B * NK * 56 * sizeof(double), h->stream));
+  HIPCHK(hipMemsetAsync(d.du, 0, B * NK * 4 * sizeof(double), h->stream));
+  HIPCHK(hipMemsetAsync(d.G, 0, B * NK * 14 * sizeof(double), h->stream));
+  HIPCHK(launch_init(sp, d, h->stream));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_initialize(mhpc_handle* h) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->x0_set) return fail(MHPC_ERR_STATE, "mhpc_set_x0 must precede mhpc_initialize");
+  HIPCHK(hipSetDevice(h->device));
+  int rc = initialize_async(h);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->initialized = true;
+  h->solved = false;
+  return MHPC_OK;
+}
+
+// MultiPhaseDDP::solve (MultiPhaseDDP.cpp:154-289) as a fixed launch schedule; every kernel
+// skips the problems whose device state machine has left the corresponding loop.
+static int solve_async(mhpc_handle* h) {
+  const SolveParams& sp = h->sp;
+  const DevBufs& d = h->d;
+  const mhpc_hsddp_option& o = h->opt;
+  int n_al = 0;
+  for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
+  for (int al = 1; al <= o.max_AL_iter; ++al) {
+    HIPCHK(launch_rollout(sp, d, 1, al, 0, 0, h->stream));  // forward_sweep(0)
+    HIPCHK(launch_partials(sp, d, h->stream));
+    int max_ddp = 0;
+    for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
+    for (int ddp = 1; ddp <= max_ddp; ++ddp) {
+      HIPCHK(launch_bws(sp, d, o.update_regularization, h->stream));
+      HIPCHK(launch_rollout(sp, d, 0, al, ddp, max_ddp, h->stream));  // forward_iteration
+      if (ddp < max_ddp) HIPCHK(launch_partials(sp, d, h->stream));
+    }
+    HIPCHK(launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
+  }
+  if (n_al == 0) HIPCHK(launch_al_end(sp, d, 1, h->stream));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "mhpc_initialize must precede mhpc_solve");
+  if (h->solved) return fail(MHPC_ERR_STATE, "solve already ran: call mhpc_initialize again");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipEventRecord(h->ev0, h->stream));
+  int rc = solve_async(h);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(h->ev1, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipEventElapsedTime(&h->solve_ms, h->ev0, h->ev1));
+  h->solved = true;
+  if (status) {
+    std::vector<ProbState> st(h->sp.B);
+    HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
+    for (int b = 0; b < h->sp.B; ++b) status[b] = st[b].status;
+  }
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y,
+                              double* K, double* du, double* Vx) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+  const SolveParams& sp = h->sp;
+  if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
+  HIPCHK(hipSetDevice(h->device));
+  const size_t B = sp.B, NK = sp.NK;
+  const int n = sp.xs[phase], N = sp.N[phase], ko = sp.ko[phase];
+  if (x || u || y) {
+    HIPCHK(launch_export(sp, h->d, h->stream));
+    std::vector<double> buf(B * NK * KS);
+    HIPCHK(hipMemcpyAsync(buf.data(), h->d.out, buf.size() * sizeof(double), hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (size_t b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k) {
+        const double* r = &buf[(b * NK + ko + k) * KS];
+        for (int i = 0; i < n; ++i)
+          if (x) x[(b * N + k) * n + i] = r[i];
+        for (int i = 0; i < 4; ++i) {
+          if (u) u[(b * N + k) * 4 + i] = r[n + i];
+          if (y) y[(b * N + k) * 4 + i] = r[n + 4 + i];
+        }
+      }
+  }
+  if (K) {
+    std::vector<double> buf(B * NK * 56);
+    HIPCHK(hipMemcpy(buf.data(), h->d.K, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k)
+        memcpy(&K[(b * N + k) * 4 * n], &buf[(b * NK + ko + k) * 56], 4 * n * sizeof(double));
+  }
+  if (du) {
+    std::vector<double> buf(B * NK * 4);
+    HIPCHK(hipMemcpy(buf.data(), h->d.du, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k) memcpy(&du[(b * N + k) * 4], &buf[(b * NK + ko + k) * 4], 4 * sizeof(double));
+  }
+  if (Vx) {
+    std::vector<double> buf(B * NK * 14);
+    HIPCHK(hipMemcpy(buf.data(), h->d.G, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k)
+        memcpy(&Vx[(b * N + k) * n], &buf[(b * NK + ko + k) * 14], n * sizeof(double));
+  }
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol,
+                                double* V_phase, double* dV_phase, int32_t* trace) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+  HIPCHK(hipSetDevice(h->device));
+  const SolveParams& sp = h->sp;
+  std::vector<ProbState> st(sp.B);
+  HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
+  for (int b = 0; b < sp.B; ++b) {
+    if (J) J[b] = st[b].J;
+    if (dV_exp) dV_exp[b] = st[b].dV_exp;
+    if (viol) viol[b] = st[b].viol;
+    for (int p = 0; p < sp.P; ++p) {
+      if (V_phase) V_phase[b * sp.P + p] = st[b].V[p];
+      if (dV_phase) dV_phase[b * sp.P + p] = st[b].dV[p];
+    }
+    if (trace) memcpy(&trace[(size_t)b * TRACE], st[b].trace, TRACE * sizeof(int32_t));
+  }
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) {
+  if (!h || !c) return fail(MHPC_ERR_INVALID, "null argument");
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<ProbState> st(h->sp.B);
+  HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
+  memset(c, 0, sizeof *c);
+  for (const ProbState& s : st) {
+    c->ddp_iters += s.cnt[C_DDP];
+    c->bws_sweeps += s.cnt[C_BWS];
+    c->bws_knots += s.cnt[C_BWS_KNOTS];
+    c->ls_rollouts += s.cnt[C_LS];
+    c->fwd_sweeps += s.cnt[C_FWD];
+    c->partial_sweeps += s.cnt[C_PAR];
+  }
+  c->solve_ms = h->solve_ms;
+  return MHPC_OK;
+}
+
+extern "C" void mhpc_destroy(mhpc_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_bufs(h);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+// ---- batched model evaluation hooks ---------------------------------------------------------
+namespace {
+struct DevScratch {
+  std::vector<void*> ptrs;
+  ~DevScratch() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  double* put(const double* host, size_t n, hipError_t* e) {
+    void* p = nullptr;
+    if (*e == hipSuccess) *e = hipMalloc(&p, n * sizeof(double) + 8);
+    if (*e == hipSuccess) ptrs.push_back(p);
+    if (*e == hipSuccess && host) *e = hipMemcpy(p, host, n * sizeof(double), hipMemcpyHostToDevice);
+    return (double*)p;
+  }
+};
+}  // namespace
+
+extern "C" int mhpc_eval_wb_dynamics(int device, int n, int mode, const double* x, const double* u,
+                                     double* xdot, double* y) {
+  if (n < 1 || !x || !u || !xdot || !y || mode < 1 || mode > 4)
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 14, &e), *du = s.put(u, n * 4, &e);
+  double *dxd = s.put(nullptr, n * 14, &e), *dy = s.put(nullptr, n * 4, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_wb_dyn(n, mode, dx, du, dxd, dy, nullptr));
+  HIPCHK(hipMemcpy(xdot, dxd, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(y, dy, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_eval_wb_partials(int device, int n, int mode, const double* x, const double* u,
+                                     double* Ac, double* Bc, double* C, double* D) {
+  if (n < 1 || !x || !u || !Ac || !Bc || !C || !D || mode < 1 || mode > 4)
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 14, &e), *du = s.put(u, n * 4, &e);
+  double *dA = s.put(nullptr, n * 196, &e), *dB = s.put(nullptr, n * 56, &e);
+  double *dC = s.put(nullptr, n * 56, &e), *dD = s.put(nullptr, n * 16, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_wb_par(n, mode, dx, du, dA, dB, dC, dD, nullptr));
+  HIPCHK(hipMemcpy(Ac, dA, n * 196 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Bc, dB, n * 56 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(C, dC, n * 56 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(D, dD, n * 16 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_eval_wb_impact(int device, int n, int foot, const double* x, double* xplus,
+                                   double* Px) {
+  if (n < 1 || !x || !xplus || !Px || (foot != 0 && foot != 1))
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 14, &e), *dxp = s.put(nullptr, n * 14, &e);
+  double* dP = s.put(nullptr, n * 196, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_wb_impact(n, foot, dx, dxp, dP, nullptr));
+  HIPCHK(hipMemcpy(xplus, dxp, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Px, dP, n * 196 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_eval_srb(int device, int n, const double* x, const double* u,
+                             const double* foothold, const double* contact, double* xdot,
+                             double* Ac, double* Bc) {
+  if (n < 1 || !x || !u || !foothold || !contact || !xdot || !Ac || !Bc)
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 6, &e), *du = s.put(u, n * 4, &e), *dp = s.put(foothold, n * 4, &e);
+  double *dc = s.put(contact, n * 2, &e), *dxd = s.put(nullptr, n * 6, &e);
+  double *dA = s.put(nullptr, n * 36, &e), *dB = s.put(nullptr, n * 24, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_srb(n, dx, du, dp, dc, dxd, dA, dB, nullptr));
+  HIPCHK(hipMemcpy(xdot, dxd, n * 6 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Ac, dA, n * 36 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Bc, dB, n * 24 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}

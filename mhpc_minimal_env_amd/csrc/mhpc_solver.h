@@ -1,0 +1,89 @@
+// Device-side data model of the batched HSDDP solve (shared by kernels and runtime).
+//
+// HBM layout (one handle = one batch of B problems sharing a phase layout; every array is
+// problem-major so each problem's records are contiguous and a wave's loads of one knot
+// record are coalesced):
+//   traj   [B][NSLOT][NK][KS]  x(<=14) u(4) y(4) per knot, KS = 24 doubles.  NSLOT =
+//          n_cand + 1 rollout slots; state.nom_slot names the nominal trajectory and the
+//          line-search candidates write the other slots (no copy on acceptance).
+//   refpos [B][NK]             forward position reference (ReferenceGen.h:94-109); the
+//          rest of the reference is constant per mode and computed in registers.
+//   K      [B][NK][56], du [B][NK][4], G [B][NK][14]   CostToGoStruct outputs per knot.
+//   par    [B][NK][PS]         dynamics Jacobians of the nominal trajectory, PS = 162 =
+//          18 tangent directions x (7 qddot rows + 2 contact-force rows) per WB knot
+//          (SRB knots are differentiated in registers by the backward kernel).
+//   px     [B][P][196]         impact Jacobian Px (column-major) at the end of WB phases.
+//   state  [B]                 ProbState (control flow + AL/ReB parameters).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mhpc_capi.h"
+
+namespace mhpc {
+
+constexpr int KS = 24;        // doubles per knot record in traj
+constexpr int PS = 162;       // doubles per knot in par
+constexpr int MAXP = MHPC_MAX_PHASES;
+constexpr int MAXC = 32;      // max line-search candidates
+constexpr int TRACE = MHPC_TRACE_LEN;
+
+// Counter slots of ProbState::cnt
+enum { C_DDP = 0, C_BWS, C_BWS_KNOTS, C_LS, C_FWD, C_PAR, C_LS_RUN, C_PAR_RUN, NCNT };
+
+struct SolveParams {
+  int B, P, n_wb, NK;
+  int mode[MAXP], N[MAXP], ko[MAXP], xs[MAXP];
+  double dt[MAXP];
+  double vel, height;
+  int n_cand, nslot;
+  double eps[MAXC];          // line-search grid 1, alpha, alpha^2, ... (host libm)
+  double gamma, DDP_thresh, AL_thresh, update_penalty, update_relax, update_regularization,
+      update_ReB;
+  double eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
+  int AL_active, ReB_active;
+  int par_items;             // partials work items per problem
+  int par_item_off[MAXP + 1];  // prefix offsets of partials items per phase
+};
+
+struct ProbState {
+  double J, viol, dV_exp, reg, cost_prev;
+  double V[MAXP], dV[MAXP], h[MAXP];
+  double sigma[MAXP], lambda[MAXP], delta[MAXP], eps_tq[MAXP], eps_grf[MAXP];
+  int32_t status;      // mhpc_solve_status
+  int32_t active;      // still inside the AL loop
+  int32_t ddp_active;  // still inside the DDP loop of this AL iteration
+  int32_t reb_active;  // _option.ReB_active of this AL iteration
+  int32_t al_partials; // terminal AL partials present (B1: only after forward_sweep(0))
+  int32_t nom_slot;
+  int32_t al_iter, ddp_iter;
+  int32_t bws_iter;    // backward sweeps of this DDP iteration
+  int32_t ntrace;
+  int32_t trace[TRACE];
+  int64_t cnt[NCNT];
+};
+
+struct DevBufs {
+  double* traj;
+  double* refpos;
+  double* K;
+  double* du;
+  double* G;
+  double* par;
+  double* px;
+  double* x0;
+  ProbState* st;
+  double* out;    // export staging [B][NK][KS]
+};
+
+// ---- cost weights (MHPCCost.cpp:24-75) and constraint constants (MHPCConstraints.cpp) --
+#if defined(__HIPCC__)
+#define MHPC_CONST __constant__
+#else
+#define MHPC_CONST static const
+#endif
+
+struct Weights {
+  double Q[4][14], R[4][4], S[4][4], Qf[4][14];
+};
+
+}  // namespace mhpc

@@ -1,0 +1,303 @@
+"""Host-side mirror of the reference's MHPC controller surface.
+
+Same names, fields, defaults and argument meaning as the reference's C++ API:
+  HSDDP_OPTION          MHPC_CompoundTypes.h:196-212
+  USRCMD                MHPC_CompoundTypes.h:237-240
+  MHPCUserParameters    MHPC_CompoundTypes.h:242-251   (alias MHPC_UserParameter)
+  GaitType2D / Gait     Common/header/Gait.h:6-77
+  MHPCLocomotion        Controller/MHPCLocomotion/MHPCLocomotion.{h,cpp}
+but one MHPCLocomotion object drives a BATCH of independent problems on one GPU through
+the C-ABI (include/mhpc_capi.h).  Numbers come only from the HIP library; there is no CPU
+fallback in this module.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import List, Optional
+
+import numpy as np
+
+from . import capi
+
+PI = 3.141592653589793238  # MHPC_CPPTypes.h:18
+
+
+def f32(v: float) -> float:
+    """A reference `float` parameter promoted to double."""
+    return float(np.float32(v))
+
+
+# ----------------------------------------------------------------------------------------
+@dataclass
+class HSDDP_OPTION:
+    alpha: float = 0.1
+    gamma: float = 0.01
+    update_penalty: float = 8
+    update_relax: float = 0.1
+    update_regularization: float = 2
+    update_ReB: float = 7
+    max_DDP_iter: float = 3
+    max_AL_iter: float = 2
+    DDP_thresh: float = 1e-03
+    AL_thresh: float = 1e-03
+    AL_active: bool = True
+    ReB_active: bool = True
+    smooth_active: bool = False
+
+    def to_c(self) -> capi.HsddpOption:
+        o = capi.HsddpOption()
+        for k in ("alpha", "gamma", "update_penalty", "update_relax", "update_regularization",
+                  "update_ReB", "max_DDP_iter", "max_AL_iter", "DDP_thresh", "AL_thresh"):
+            setattr(o, k, float(getattr(self, k)))
+        o.AL_active = int(bool(self.AL_active))
+        o.ReB_active = int(bool(self.ReB_active))
+        o.smooth_active = int(bool(self.smooth_active))
+        return o
+
+
+@dataclass
+class USRCMD:
+    vel: float = 0.0
+    height: float = 0.0
+    roll: float = 0.0
+    pitch: float = 0.0
+    yaw: float = 0.0
+
+
+@dataclass
+class MHPCUserParameters:
+    n_wbphase: int = 4
+    n_fbphase: int = 4
+    dt_wb: float = .001
+    dt_fb: float = .001
+    cmode: int = 1
+    groundH: float = -0.404  # unused by the reference too (ground hard-coded)
+    usrcmd: Optional[USRCMD] = None
+
+
+MHPC_UserParameter = MHPCUserParameters  # the north star's spelling
+
+
+class GaitType2D(Enum):
+    STAND = 0
+    BOUND = 1
+    PRONK = 2
+
+
+class Gait:
+    """Gait.h:13-77.  Only BOUND is defined; every other type takes the default branch
+    (uniform 0.08 s timings) exactly as the reference's switch does."""
+
+    def __init__(self, gait: Optional[GaitType2D] = None):
+        self._gait_mode = [1, 2, 3, 4]
+        self._gait_name = "BOUND"
+        if gait is None or gait == GaitType2D.BOUND:
+            self._gait_timing = [f32(0.08), f32(0.1), f32(0.08), f32(0.1)]
+        else:
+            self._gait_timing = [f32(0.08)] * 4
+
+    def get_next_mode(self, current_mode: int) -> int:
+        for idx, m in enumerate(self._gait_mode):
+            if m == current_mode:
+                return self._gait_mode[(idx + 1) % len(self._gait_mode)]
+        raise ValueError(f"mode {current_mode} not in gait")
+
+    def get_mode_seq(self, current_mode: int, num_phases: int) -> List[int]:
+        assert num_phases >= 1
+        seq = [current_mode]
+        for _ in range(num_phases - 1):
+            seq.append(self.get_next_mode(seq[-1]))
+        return seq
+
+    def get_timings(self, mode_seq: List[int]) -> List[float]:
+        return [self._gait_timing[m - 1] for m in mode_seq]
+
+
+def c_round(v: float) -> int:
+    """C `round()` (half away from zero)."""
+    return int(math.floor(abs(v) + 0.5)) * (1 if v >= 0 else -1)
+
+
+def make_problem_desc(n_wb: int, n_fb: int, mode_seq: List[int], timings: List[float],
+                      dt_wb: float, dt_fb: float, vel: float, height: float = 0.0,
+                      N: Optional[List[int]] = None) -> capi.ProblemDesc:
+    """MHPCLocomotion::build_problem (MHPCLocomotion.cpp:63-104): N = round(timing / dt)
+    with float timings and float dt promoted to double."""
+    d = capi.ProblemDesc()
+    np_ = n_wb + n_fb
+    if not 1 <= np_ <= capi.MHPC_MAX_PHASES:
+        raise ValueError("number of phases out of range")
+    d.n_wb, d.n_fb = n_wb, n_fb
+    d.dt_wb, d.dt_fb = f32(dt_wb), f32(dt_fb)
+    for p in range(np_):
+        d.mode_seq[p] = mode_seq[p]
+        if N is not None:
+            d.N[p] = N[p]
+        else:
+            dt = d.dt_wb if p < n_wb else d.dt_fb
+            d.N[p] = c_round(f32(timings[p]) / dt)
+    d.vel_cmd = f32(vel)
+    d.height_cmd = f32(height)
+    d.precision = 64
+    return d
+
+
+def desc_from_params(params: MHPCUserParameters, gait: Gait) -> capi.ProblemDesc:
+    n = params.n_wbphase + params.n_fbphase
+    seq = gait.get_mode_seq(params.cmode, n)
+    cmd = params.usrcmd or USRCMD()
+    return make_problem_desc(params.n_wbphase, params.n_fbphase, seq, gait.get_timings(seq),
+                             params.dt_wb, params.dt_fb, cmd.vel, cmd.height)
+
+
+# Default initial condition (MHPCLocomotion.cpp:37-39)
+Q0 = np.array([0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098])
+QD0 = np.array([0.9011, 0.2756, 0.7333, 0.0446, 0.0009, 1.3219, 2.7346])
+X0_DEFAULT = np.concatenate([Q0, QD0])
+STATE_PROJ_ROWS = [0, 1, 2, 7, 8, 9]  # _stateProj (MHPCLocomotion.cpp:32-34)
+
+X0_SEED = 0x4D485043
+_X0_AMP = np.array([0.01, 0.01] + [0.02] * 5 + [0.05] * 7)
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(state: int):
+    state = (state + 0x9E3779B97F4A7C15) & _M64
+    z = state
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return state, z ^ (z >> 31)
+
+
+def random_x0(batch: int, seed: int = X0_SEED, offset: int = 0) -> np.ndarray:
+    """x0_b = x0_default + delta_b.  Problem b draws from its own
+    splitmix64 stream, state0 = seed ^ (b * 0xD1B54A32D192ED03); U = (next >> 11) * 2^-53,
+    delta = amp * (2U - 1).  `offset` = global index of the first problem (sharding)."""
+    out = np.empty((batch, 14))
+    for i in range(batch):
+        b = offset + i
+        st = (seed ^ ((b * 0xD1B54A32D192ED03) & _M64)) & _M64
+        for j in range(14):
+            st, z = _splitmix64(st)
+            U = (z >> 11) * (1.0 / (1 << 53))
+            out[i, j] = X0_DEFAULT[j] + _X0_AMP[j] * (2 * U - 1)
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+class MHPCLocomotion:
+    """Batched MHPCLocomotion<double> over the C-ABI.
+
+    MHPCLocomotion(params, gait, option)               (MHPCLocomotion.cpp:8-43)
+    .initialization()                                    (:47-53)
+    .solve_mhpc()                                        (:167-195)
+    .print_debugInfo(dirname)                            (:293-380)
+    Extensions: `batch`, `set_initial_condition(x0[batch][n])` before initialization
+    (the reference always starts from its private default x0), `desc=` for layouts the
+    reference's constructor cannot express (SRB-only C1, N > 110 C2)."""
+
+    def __init__(self, params: Optional[MHPCUserParameters] = None, gait: Optional[Gait] = None,
+                 option: Optional[HSDDP_OPTION] = None, batch: int = 1, device: int = 0,
+                 desc: Optional[capi.ProblemDesc] = None):
+        self.params = params or MHPCUserParameters(usrcmd=USRCMD(vel=1.5))
+        self.gait = gait or Gait()
+        self.option = option or HSDDP_OPTION()
+        self.desc = desc if desc is not None else desc_from_params(self.params, self.gait)
+        self.batch = int(batch)
+        self.device = int(device)
+        self._opt_c = self.option.to_c()
+        L = capi.lib()
+        h = __import__("ctypes").c_void_p()
+        capi.check(L.mhpc_create(self.desc, self._opt_c, self.batch, self.device,
+                                 __import__("ctypes").byref(h)), "mhpc_create")
+        self._h = h
+        n0 = self.desc.xsize(0)
+        x0 = X0_DEFAULT if n0 == 14 else X0_DEFAULT[STATE_PROJ_ROWS]
+        self._x0 = np.tile(x0, (self.batch, 1)).astype(np.float64)
+        self.status = np.zeros(self.batch, dtype=np.int32)
+
+    # -- lifecycle ---------------------------------------------------------------------
+    def set_initial_condition(self, x0: np.ndarray):
+        x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(self.batch, -1))
+        if x0.shape[1] != self.desc.xsize(0):
+            raise ValueError("x0 has the wrong state size for phase 0")
+        self._x0 = x0
+
+    def initialization(self):
+        L = capi.lib()
+        capi.check(L.mhpc_set_x0(self._h, capi.dptr(self._x0)), "mhpc_set_x0")
+        capi.check(L.mhpc_initialize(self._h), "mhpc_initialize")
+
+    def solve_mhpc(self) -> np.ndarray:
+        capi.check(capi.lib().mhpc_solve(self._h, capi.iptr(self.status)), "mhpc_solve")
+        return self.status
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            capi.lib().mhpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- outputs -----------------------------------------------------------------------
+    def get_phase(self, p: int) -> dict:
+        n, N, B = self.desc.xsize(p), self.desc.N[p], self.batch
+        out = {k: np.zeros(s) for k, s in (
+            ("x", (B, N, n)), ("u", (B, N, 4)), ("y", (B, N, 4)), ("K", (B, N, 4, n)),
+            ("du", (B, N, 4)), ("Vx", (B, N, n)))}
+        capi.check(capi.lib().mhpc_get_phase(
+            self._h, p, *[capi.dptr(out[k]) for k in ("x", "u", "y", "K", "du", "Vx")]),
+            "mhpc_get_phase")
+        return out
+
+    def get_scalars(self) -> dict:
+        B, P = self.batch, self.desc.n_phases
+        out = {"J": np.zeros(B), "dV_exp": np.zeros(B), "viol": np.zeros(B),
+               "V": np.zeros((B, P)), "dV": np.zeros((B, P)),
+               "trace": np.zeros((B, capi.MHPC_TRACE_LEN), dtype=np.int32)}
+        capi.check(capi.lib().mhpc_get_scalars(
+            self._h, capi.dptr(out["J"]), capi.dptr(out["dV_exp"]), capi.dptr(out["viol"]),
+            capi.dptr(out["V"]), capi.dptr(out["dV"]), capi.iptr(out["trace"])),
+            "mhpc_get_scalars")
+        return out
+
+    def get_counters(self) -> dict:
+        c = capi.Counters()
+        capi.check(capi.lib().mhpc_get_counters(self._h, __import__("ctypes").byref(c)),
+                   "mhpc_get_counters")
+        return {k: getattr(c, k) for k, _ in capi.Counters._fields_}
+
+    def concatenated(self) -> dict:
+        """Phase-concatenated per-problem arrays (the oracle's layout)."""
+        parts = [self.get_phase(p) for p in range(self.desc.n_phases)]
+        B = self.batch
+        return {
+            "X": np.concatenate([q["x"].reshape(B, -1) for q in parts], axis=1),
+            "U": np.concatenate([q["u"].reshape(B, -1) for q in parts], axis=1),
+            "Y": np.concatenate([q["y"].reshape(B, -1) for q in parts], axis=1),
+            "K": np.concatenate([q["K"].reshape(B, -1) for q in parts], axis=1),
+            "DU": np.concatenate([q["du"].reshape(B, -1) for q in parts], axis=1),
+            "G": np.concatenate([q["Vx"].reshape(B, -1) for q in parts], axis=1),
+        }
+
+    def print_debugInfo(self, dirname: str = ".", problem: int = 0):
+        """state.txt / control.txt / gradient.txt of one problem (MHPCLocomotion.cpp:293-380,
+        without the reference's [i+2] indexing bug for n_wbphase != 2)."""
+        os.makedirs(dirname, exist_ok=True)
+        parts = [self.get_phase(p) for p in range(self.desc.n_phases)]
+
+        def dump(fname, key):
+            with open(os.path.join(dirname, fname), "w") as f:
+                for q in parts:
+                    for row in q[key][problem]:
+                        f.write(" ".join(f"{v:.6g}" for v in np.ravel(row)) + "\n")
+        dump("state.txt", "x")
+        dump("control.txt", "u")
+        dump("gradient.txt", "Vx")

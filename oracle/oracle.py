@@ -1,0 +1,97 @@
+"""TEST INFRASTRUCTURE ONLY -- Python access to the CPU oracle (oracle/hsddp_oracle.cpp).
+
+The oracle restates the reference HSDDP solve line by line (citations in the .cpp) and
+evaluates every model function with the reference's own CasADi kernels
+(oracle/_ref/libmhpc_casadi_ref.so, built from /root/reference/CasadiGen/source).  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+ORACLE_SO = os.path.join(HERE, "_build", "libmhpc_oracle.so")
+sys.path.insert(0, HERE)
+import casadi_ref  # noqa: E402
+
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+from mhpc_minimal_env_amd import capi  # noqa: E402  (struct definitions of the boundary only)
+
+TRACE_LEN = capi.MHPC_TRACE_LEN
+_lib = None
+
+
+def build(quiet: bool = True) -> bool:
+    """Compile the oracle (and, when /root/reference is present, the CasADi reference)."""
+    targets = ["oracle"] + (["ref"] if os.path.isdir("/root/reference/CasadiGen/source") else [])
+    r = subprocess.run(["make", "-C", HERE] + targets, capture_output=quiet, text=True)
+    return r.returncode == 0
+
+
+def available() -> bool:
+    return os.path.exists(ORACLE_SO) and casadi_ref.available()
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not available():
+            raise FileNotFoundError("oracle or CasADi reference library not built")
+        L = ctypes.CDLL(ORACLE_SO)
+        L.oracle_load_ref.argtypes = [ctypes.c_char_p]
+        L.oracle_solve.restype = ctypes.c_int
+        rc = L.oracle_load_ref(casadi_ref.REF_SO.encode())
+        if rc != 0:
+            raise RuntimeError(f"oracle_load_ref failed ({rc})")
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def solve(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray, nthreads: int = 1,
+          do_solve: bool = True) -> dict:
+    """Run the oracle on x0 [batch][n0]; returns phase-concatenated outputs (see
+    oracle/mhpc_oracle.h)."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B = x0.shape[0]
+    lx, lu, lk = desc.lens()
+    P = desc.n_phases
+    out = {
+        "X": np.zeros((B, lx)), "U": np.zeros((B, lu)), "Y": np.zeros((B, lu)),
+        "K": np.zeros((B, lk)), "DU": np.zeros((B, lu)), "G": np.zeros((B, lx)),
+        "J": np.zeros(B), "dV_exp": np.zeros(B), "viol": np.zeros(B),
+        "V": np.zeros((B, P)), "dV": np.zeros((B, P)),
+        "status": np.zeros(B, dtype=np.int32),
+        "trace": np.zeros((B, TRACE_LEN), dtype=np.int32),
+        "counters": np.zeros((B, 6), dtype=np.int64),
+    }
+    rc = lib().oracle_solve(
+        ctypes.byref(desc), ctypes.byref(opt), ctypes.c_int(B), _p(x0), ctypes.c_int(nthreads),
+        ctypes.c_int(1 if do_solve else 0),
+        *[_p(out[k]) for k in ("X", "U", "Y", "K", "DU", "G", "J", "dV_exp", "viol", "V", "dV",
+                               "status", "trace", "counters")])
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve failed ({rc})")
+    return out
+
+
+def decode_trace(t) -> list:
+    """Decision trace entries -> dicts (encoding: DESIGN.md §Parity)."""
+    res = []
+    for v in t:
+        v = int(v)
+        if v < 0:
+            break
+        res.append({"al": v >> 24, "reb": (v >> 23) & 1, "conv": (v >> 22) & 1,
+                    "abort": (v >> 21) & 1, "n_ls": (v >> 8) & 0xFF, "n_bws": v & 0xFF})
+    return res

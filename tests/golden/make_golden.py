@@ -1,0 +1,108 @@
+"""Generate the committed golden fixtures (run in the container that holds /root/reference).
+
+  kat_model.npz      per-function known-answer vectors of the reference's OWN CasADi kernels
+                     (oracle/_ref, compiled from /root/reference/CasadiGen/source): random
+                     (x, u) per mode, x ~ U(-1,1) for q and U(-3,3) for qdot, u ~ U(-20,20)
+                     (SURVEY.md §8c(i)); dense outputs scattered like casadi_interface.
+  solve_<cfg>.npz    full HSDDP solves of the CPU oracle (restatement + CasADi kernels) for
+                     the BASELINE configs at small batch: inputs (x0) and every output incl.
+                     the decision trace.
+
+The reference cannot travel to the GPU box, so these files are what the GPU tests check
+against when the oracle cannot run there.  Usage: python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+
+import casadi_ref as cr  # noqa: E402
+import oracle as O  # noqa: E402
+from mhpc_minimal_env_amd import configs, locomotion as L  # noqa: E402
+
+KAT_N = 64
+KAT_SEED = 20261015
+
+
+def make_kat():
+    rng = np.random.default_rng(KAT_SEED)
+    n = KAT_N
+    x = np.concatenate([rng.uniform(-1, 1, (n, 7)), rng.uniform(-3, 3, (n, 7))], axis=1)
+    u = rng.uniform(-20, 20, (n, 4))
+    out = {"x": x, "u": u}
+    for nm in ("Dyn_BS", "Dyn_FL", "Dyn_FS"):
+        r = [cr.call(nm, x[i], u[i]) for i in range(n)]
+        out[nm + ".xdot"] = np.stack([a[0] for a in r])
+        out[nm + ".y"] = np.stack([a[1] for a in r])
+        r = [cr.call(nm + "_par", x[i], u[i]) for i in range(n)]
+        for j, k in enumerate(("Ac", "Bc", "C", "D")):
+            out[f"{nm}_par.{k}"] = np.stack([a[j] for a in r])
+    for nm in ("Imp_F", "Imp_B"):
+        r = [cr.call(nm, x[i]) for i in range(n)]
+        out[nm + ".xplus"] = np.stack([a[0] for a in r])
+        out[nm + ".y"] = np.stack([a[1] for a in r])
+        out[nm + "_par.Px"] = np.stack([cr.call(nm + "_par", x[i])[0] for i in range(n)])
+    for nm in ("WB_FL1_terminal_constr", "WB_FL2_terminal_constr"):
+        r = [cr.call(nm, x[i]) for i in range(n)]
+        out[nm + ".h"] = np.array([np.ravel(a[0])[0] for a in r])
+        out[nm + ".hx"] = np.stack([np.ravel(a[1]) for a in r])
+        out[nm + ".hxx"] = np.stack([a[2] for a in r])
+    for nm in ("Jacob_F", "Jacob_B"):
+        r = [cr.call(nm, x[i]) for i in range(n)]
+        out[nm + ".J"] = np.stack([a[0] for a in r])
+        out[nm + ".Jd"] = np.stack([a[1] for a in r])
+    xs = rng.uniform(-1, 1, (n, 6))
+    us = rng.uniform(-50, 50, (n, 4))
+    ps = rng.uniform(-1, 1, (n, 4))
+    ss = np.array([[0, 1], [1, 0], [0, 0], [1, 1]] * (n // 4), dtype=float)
+    out.update({"srb.x": xs, "srb.u": us, "srb.p": ps, "srb.s": ss})
+    r = [cr.call("FBDynamics", xs[i], us[i], ps[i], ss[i]) for i in range(n)]
+    out["FBDynamics.xdot"] = np.stack([a[0] for a in r])
+    r = [cr.call("FBDynamics_par", xs[i], us[i], ps[i], ss[i]) for i in range(n)]
+    out["FBDynamics_par.Ac"] = np.stack([a[0] for a in r])
+    out["FBDynamics_par.Bc"] = np.stack([a[1] for a in r])
+    return out
+
+
+SOLVES = {
+    # name: (desc factory, batch)
+    "c1": (configs.c1_desc, 2),
+    "c2": (configs.c2_desc, 2),
+    "c3": (configs.c3_desc, 8),
+    "c5": (configs.c5_desc, 2),
+}
+
+
+def make_solve(name):
+    fn, B = SOLVES[name]
+    desc = fn()
+    opt = L.HSDDP_OPTION()
+    x0 = configs.x0_for(desc, B)
+    res = O.solve(desc, opt.to_c(), x0, nthreads=4)
+    res["x0"] = x0
+    res["desc"] = np.array(str(desc.describe()))
+    return res
+
+
+def main():
+    assert O.available(), "build the oracle and oracle/_ref first (make -C oracle)"
+    np.savez_compressed(os.path.join(HERE, "kat_model.npz"), **make_kat())
+    for name in SOLVES:
+        np.savez_compressed(os.path.join(HERE, f"solve_{name}.npz"), **make_solve(name))
+    # smoke fixture: first 4 problems of C3 (same x0 stream as __graft_entry__.smoke)
+    desc = configs.c3_desc()
+    x0 = L.random_x0(4)
+    res = O.solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=4)
+    res["x0"] = x0
+    np.savez_compressed(os.path.join(HERE, "smoke_c3_b4.npz"), **res)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
