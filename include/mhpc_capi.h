@@ -128,6 +128,16 @@ int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, d
 int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
                      double* dV_phase, int32_t* trace);
 int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
+
+/* Per-kernel device timing (HIP events around every launch on the handle's stream) and the
+ * algorithmic HBM bytes each kernel must move (model in DESIGN.md §Roofline), accumulated
+ * over all solves since the last reset.  Kernel ids: 0 init, 1 rollout_full,
+ * 2 rollout_linesearch, 3 partials, 4 backward_sweep, 5 al_update. */
+#define MHPC_NUM_KERNELS 6
+const char* mhpc_kernel_name(int k);
+int mhpc_set_profiling(mhpc_handle* h, int on);
+int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches, double* alg_bytes);
+int mhpc_reset_kernel_stats(mhpc_handle* h);
 void mhpc_destroy(mhpc_handle* h);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

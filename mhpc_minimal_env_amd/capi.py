@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libmhpc_amd.so")
 MHPC_MAX_PHASES = 16
 MHPC_MAX_KNOTS = 1024
 MHPC_TRACE_LEN = 64
+MHPC_NUM_KERNELS = 6
 
 MHPC_OK = 0
 MHPC_SOLVE_OK = 0
@@ -112,6 +113,11 @@ SIGNATURES = [
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),
+    ("mhpc_kernel_name", ctypes.c_char_p, [ctypes.c_int]),
+    ("mhpc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("mhpc_get_kernel_stats", ctypes.c_int, [ctypes.c_void_p, _DP,
+                                             ctypes.POINTER(ctypes.c_int64), _DP]),
+    ("mhpc_reset_kernel_stats", ctypes.c_int, [ctypes.c_void_p]),
     ("mhpc_eval_wb_dynamics", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                              _DP, _DP]),
     ("mhpc_eval_wb_partials", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,

@@ -332,6 +332,7 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
                                   ((nls & 0xff) << 8) | (st->bws_iter & 0xff);
       st->cnt[C_LS] += nls < nc ? nls : nc;
       st->cnt[C_LS_RUN] += nc;
+      st->cnt[C_LS_LAUNCH]++;
       if (conv) {
         st->ddp_active = 0;
       } else {
@@ -742,7 +743,8 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
 }
 
 __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st,
-                          BwsLds& sh, double reg, int64_t* knots) {
+                          BwsLds& sh, double reg, int64_t* knots, int64_t* knots_wb,
+                          int64_t* px_reads) {
   const int lane = threadIdx.x;
   const int nom = st->nom_slot;
   double dVnext = 0;
@@ -763,6 +765,7 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
         if (imp) {
           const double* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
           for (int e = lane; e < 196; e += 64) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
+          ++*px_reads;
         } else {
           for (int e = lane; e < 196; e += 64) sh.Px[e] = (e / 14 == e % 14) ? 1.0 : 0.0;
         }
@@ -926,6 +929,7 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
         ok = riccati_knot<6, false>(sh, lane, lu, ly, reg, sp.eps9, Kout, duout, Gout, &dV);
       }
       ++*knots;
+      if (wb) ++*knots_wb;
       if (!ok) {
         st->dV[p] = dV;
         return false;
@@ -944,12 +948,12 @@ __global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double up
   __shared__ BwsLds sh;
   double reg = st->reg;
   int bws_iter = 1;
-  int64_t knots = 0;
+  int64_t knots = 0, knots_wb = 0, px_reads = 0;
   int64_t sweeps = 0;
   bool aborted = false;
   for (;;) {
     ++sweeps;
-    const bool ok = bws_sweep(sp, d, b, st, sh, reg, &knots);
+    const bool ok = bws_sweep(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
     if (ok) break;
     reg = fmax(reg * update_reg, 1e-03);
     ++bws_iter;
@@ -960,6 +964,9 @@ __global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double up
     st->cnt[C_DDP]++;
     st->cnt[C_BWS] += sweeps;
     st->cnt[C_BWS_KNOTS] += knots;
+    st->cnt[C_BWS_KNOTS_WB] += knots_wb;
+    st->cnt[C_BWS_KNOTS_FB] += knots - knots_wb;
+    st->cnt[C_PX_READS] += px_reads;
     st->bws_iter = bws_iter;
     if (aborted) {
       st->status = MHPC_SOLVE_REG_ABORT;
@@ -1128,7 +1135,19 @@ __global__ void k_eval_srb(int n, const double* x, const double* u, const double
   srb_jacobians(x + (size_t)i * 6, u + (size_t)i * 4, p + (size_t)i * 4, s + (size_t)i * 2, Ac + (size_t)i * 36, Bc + (size_t)i * 24);
 }
 
+// Sum the per-problem counters of the batch (int64 atomics into NCNT slots).
+__global__ void k_reduce_counters(SolveParams sp, DevBufs d, unsigned long long* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= sp.B) return;
+  for (int i = 0; i < NCNT; ++i) atomicAdd(&out[i], (unsigned long long)d.st[b].cnt[i]);
+}
+
 // ---- launchers (called by mhpc_runtime.cpp) ---------------------------------------------
+hipError_t launch_reduce_counters(const SolveParams& sp, const DevBufs& d,
+                                  unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_counters, dim3((sp.B + 255) / 256), dim3(256), 0, s, sp, d, out);
+  return hipGetLastError();
+}
 hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
   hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d);
   return hipGetLastError();

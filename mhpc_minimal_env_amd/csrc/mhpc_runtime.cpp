@@ -18,6 +18,8 @@ hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
 hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_export(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_reduce_counters(const SolveParams&, const DevBufs&, unsigned long long*,
+                                  hipStream_t);
 hipError_t launch_eval_wb_dyn(int, int, const double*, const double*, double*, double*, hipStream_t);
 hipError_t launch_eval_wb_par(int, int, const double*, const double*, double*, double*, double*,
                               double*, hipStream_t);
@@ -44,6 +46,10 @@ int fail(int code, const std::string& msg) {
   } while (0)
 }  // namespace
 
+enum { K_INIT = 0, K_FULL, K_LS, K_PAR, K_BWS, K_AL, NKERN };
+static const char* kKernelNames[NKERN] = {"k_init", "k_rollout(full)", "k_rollout(linesearch)",
+                                          "k_partials", "k_bws", "k_al_end"};
+
 struct mhpc_handle {
   mhpc_problem_desc desc;
   mhpc_hsddp_option opt;
@@ -54,7 +60,49 @@ struct mhpc_handle {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool x0_set = false, initialized = false, solved = false;
   float solve_ms = 0;
+  unsigned long long* dcnt = nullptr;  // reduced counters of the batch [NCNT]
+  unsigned long long cnt[NCNT] = {};
+  // profiling: one event pair per launch of a solve, accumulated per kernel id
+  bool profile = false;
+  std::vector<hipEvent_t> evpool;
+  std::vector<int> evkind;
+  double kms[NKERN] = {}, kbytes[NKERN] = {};
+  int64_t klaunch[NKERN] = {};
+  // algorithmic byte model per problem
+  double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0;
 };
+
+// Algorithmic HBM bytes (fp64) of one problem for each kernel's unit of work.
+static void byte_model(mhpc_handle* h) {
+  const SolveParams& sp = h->sp;
+  double rr = 14 * 8, rw = 0, pb = 0, ib = sp.NK * 8.0;
+  for (int p = 0; p < sp.P; ++p) {
+    const bool wb = p < sp.n_wb;
+    const int n = wb ? 14 : 6, N = sp.N[p];
+    // nominal x,u (n+4) + K (4n) + du (4) + refpos read once per problem
+    rr += (N - 1) * 8.0 * ((n + 4) + 4 * n + 4 + 1) + 8.0;
+    // each candidate writes x,u,y of every knot (x only at the last knot)
+    rw += (N - 1) * 8.0 * (n + 8) + n * 8.0;
+    if (wb) {
+      const bool imp = sp.mode[p] == 2 || sp.mode[p] == 4;
+      pb += (N - 1) * 8.0 * (18 + PS) + (imp ? 8.0 * (14 + 196) : 0.0);
+      ib += N * 8.0 * 22;
+    }
+  }
+  h->by_roll_read = rr;
+  h->by_roll_write = rw;
+  h->by_par = pb;
+  h->by_init = ib;
+}
+// backward sweep: per WB knot partials record + x,u,y + refpos read, K,du,G written;
+// per SRB knot x,u + refpos read, K,du,G written; Px read per impact-aware step
+static constexpr double kBwsWbKnot = 8.0 * (PS + 22 + 1 + 56 + 4 + 14);
+static constexpr double kBwsFbKnot = 8.0 * (10 + 1 + 24 + 4 + 6);
+static constexpr double kBwsPx = 8.0 * 196;
+
+extern "C" const char* mhpc_kernel_name(int k) {
+  return (k >= 0 && k < NKERN) ? kKernelNames[k] : "";
+}
 
 extern "C" const char* mhpc_version(void) { return "mhpc_minimal_env_amd 0.1 (gfx950, fp64)"; }
 extern "C" const char* mhpc_last_error(void) { return g_err.c_str(); }
@@ -172,11 +220,14 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   alloc((void**)&d.x0, B * 14 * sizeof(double));
   alloc((void**)&d.st, B * sizeof(ProbState));
   alloc((void**)&d.out, B * NK * KS * sizeof(double));
+  alloc((void**)&h->dcnt, NCNT * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
   if (e == hipSuccess) e = hipMemset(d.x0, 0, B * 14 * sizeof(double));
+  byte_model(h);
   if (e != hipSuccess) {
+    if (h->dcnt) (void)hipFree(h->dcnt);
     free_bufs(h);
     delete h;
     return fail(MHPC_ERR_DEVICE, std::string("allocation failed: ") + hipGetErrorString(e));
@@ -200,6 +251,37 @@ extern "C" int mhpc_set_x0(mhpc_handle* h, const double* x0) {
   return MHPC_OK;
 }
 
+static int mark(mhpc_handle* h, int kind) {
+  if (!h->profile) return MHPC_OK;
+  hipEvent_t e;
+  HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(e, h->stream));
+  h->evpool.push_back(e);
+  h->evkind.push_back(kind);
+  return MHPC_OK;
+}
+#define LAUNCH(h, kind, expr)          \
+  do {                                 \
+    int rc_ = mark(h, kind);           \
+    if (rc_) return rc_;               \
+    HIPCHK(expr);                      \
+    rc_ = mark(h, -1);                 \
+    if (rc_) return rc_;               \
+  } while (0)
+
+static int collect_profile(mhpc_handle* h) {
+  for (size_t i = 0; i + 1 < h->evpool.size(); i += 2) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, h->evpool[i], h->evpool[i + 1]));
+    h->kms[h->evkind[i]] += ms;
+    h->klaunch[h->evkind[i]] += 1;
+  }
+  for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
+  h->evpool.clear();
+  h->evkind.clear();
+  return MHPC_OK;
+}
+
 // initialization(): memory_reset + build_problem (refs) + warmstart, all on the device.
 static int initialize_async(mhpc_handle* h) {
   const SolveParams& sp = h->sp;
@@ -209,7 +291,8 @@ static int initialize_async(mhpc_handle* h) {
   HIPCHK(hipMemsetAsync(d.K, 0, B * NK * 56 * sizeof(double), h->stream));
   HIPCHK(hipMemsetAsync(d.du, 0, B * NK * 4 * sizeof(double), h->stream));
   HIPCHK(hipMemsetAsync(d.G, 0, B * NK * 14 * sizeof(double), h->stream));
-  HIPCHK(launch_init(sp, d, h->stream));
+  LAUNCH(h, K_INIT, launch_init(sp, d, h->stream));
+  h->kbytes[K_INIT] += h->by_init * sp.B;
   return MHPC_OK;
 }
 
@@ -220,6 +303,8 @@ extern "C" int mhpc_initialize(mhpc_handle* h) {
   int rc = initialize_async(h);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
+  rc = collect_profile(h);
+  if (rc) return rc;
   h->initialized = true;
   h->solved = false;
   return MHPC_OK;
@@ -234,18 +319,21 @@ static int solve_async(mhpc_handle* h) {
   int n_al = 0;
   for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
   for (int al = 1; al <= o.max_AL_iter; ++al) {
-    HIPCHK(launch_rollout(sp, d, 1, al, 0, 0, h->stream));  // forward_sweep(0)
-    HIPCHK(launch_partials(sp, d, h->stream));
+    LAUNCH(h, K_FULL, launch_rollout(sp, d, 1, al, 0, 0, h->stream));  // forward_sweep(0)
+    LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     int max_ddp = 0;
     for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
     for (int ddp = 1; ddp <= max_ddp; ++ddp) {
-      HIPCHK(launch_bws(sp, d, o.update_regularization, h->stream));
-      HIPCHK(launch_rollout(sp, d, 0, al, ddp, max_ddp, h->stream));  // forward_iteration
-      if (ddp < max_ddp) HIPCHK(launch_partials(sp, d, h->stream));
+      LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, h->stream));
+      LAUNCH(h, K_LS, launch_rollout(sp, d, 0, al, ddp, max_ddp, h->stream));  // forward_iteration
+      if (ddp < max_ddp) LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     }
-    HIPCHK(launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
+    LAUNCH(h, K_AL, launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
   }
-  if (n_al == 0) HIPCHK(launch_al_end(sp, d, 1, h->stream));
+  if (n_al == 0) LAUNCH(h, K_AL, launch_al_end(sp, d, 1, h->stream));
+  // batch totals of the per-problem counters (tiny reduction, NCNT words back)
+  HIPCHK(hipMemsetAsync(h->dcnt, 0, NCNT * sizeof(unsigned long long), h->stream));
+  HIPCHK(launch_reduce_counters(sp, d, h->dcnt, h->stream));
   return MHPC_OK;
 }
 
@@ -258,9 +346,19 @@ extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
   int rc = solve_async(h);
   if (rc) return rc;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
+  HIPCHK(hipMemcpyAsync(h->cnt, h->dcnt, NCNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipEventElapsedTime(&h->solve_ms, h->ev0, h->ev1));
   h->solved = true;
+  rc = collect_profile(h);
+  if (rc) return rc;
+  const unsigned long long* c = h->cnt;
+  h->kbytes[K_FULL] += c[C_FWD] * (h->by_roll_read + h->by_roll_write);
+  h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read + c[C_LS_RUN] * h->by_roll_write;
+  h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
+  h->kbytes[K_BWS] += c[C_BWS_KNOTS_WB] * kBwsWbKnot + c[C_BWS_KNOTS_FB] * kBwsFbKnot +
+                      c[C_PX_READS] * kBwsPx;
   if (status) {
     std::vector<ProbState> st(h->sp.B);
     HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
@@ -341,19 +439,37 @@ extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, doubl
 
 extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) {
   if (!h || !c) return fail(MHPC_ERR_INVALID, "null argument");
-  HIPCHK(hipSetDevice(h->device));
-  std::vector<ProbState> st(h->sp.B);
-  HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
   memset(c, 0, sizeof *c);
-  for (const ProbState& s : st) {
-    c->ddp_iters += s.cnt[C_DDP];
-    c->bws_sweeps += s.cnt[C_BWS];
-    c->bws_knots += s.cnt[C_BWS_KNOTS];
-    c->ls_rollouts += s.cnt[C_LS];
-    c->fwd_sweeps += s.cnt[C_FWD];
-    c->partial_sweeps += s.cnt[C_PAR];
-  }
+  c->ddp_iters = (int64_t)h->cnt[C_DDP];
+  c->bws_sweeps = (int64_t)h->cnt[C_BWS];
+  c->bws_knots = (int64_t)h->cnt[C_BWS_KNOTS];
+  c->ls_rollouts = (int64_t)h->cnt[C_LS];
+  c->fwd_sweeps = (int64_t)h->cnt[C_FWD];
+  c->partial_sweeps = (int64_t)h->cnt[C_PAR];
   c->solve_ms = h->solve_ms;
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_set_profiling(mhpc_handle* h, int on) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  h->profile = on != 0;
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches,
+                                     double* alg_bytes) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  for (int k = 0; k < NKERN; ++k) {
+    if (ms) ms[k] = h->kms[k];
+    if (launches) launches[k] = h->klaunch[k];
+    if (alg_bytes) alg_bytes[k] = h->kbytes[k];
+  }
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_reset_kernel_stats(mhpc_handle* h) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  for (int k = 0; k < NKERN; ++k) { h->kms[k] = 0; h->kbytes[k] = 0; h->klaunch[k] = 0; }
   return MHPC_OK;
 }
 
@@ -362,6 +478,8 @@ extern "C" void mhpc_destroy(mhpc_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_bufs(h);
+  if (h->dcnt) (void)hipFree(h->dcnt);
+  for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);

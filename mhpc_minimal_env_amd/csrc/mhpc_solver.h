@@ -27,8 +27,13 @@ constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
 constexpr int TRACE = MHPC_TRACE_LEN;
 
-// Counter slots of ProbState::cnt
-enum { C_DDP = 0, C_BWS, C_BWS_KNOTS, C_LS, C_FWD, C_PAR, C_LS_RUN, C_PAR_RUN, NCNT };
+// Counter slots of ProbState::cnt.  C_LS is the reference-equivalent number of serial
+// line-search rollouts; C_*_RUN count what this implementation actually executed; the
+// knot / Px counters feed the algorithmic-byte model of the roofline report.
+enum {
+  C_DDP = 0, C_BWS, C_BWS_KNOTS, C_LS, C_FWD, C_PAR, C_LS_RUN, C_PAR_RUN,
+  C_LS_LAUNCH, C_BWS_KNOTS_WB, C_BWS_KNOTS_FB, C_PX_READS, NCNT
+};
 
 struct SolveParams {
   int B, P, n_wb, NK;

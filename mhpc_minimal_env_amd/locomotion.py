@@ -274,6 +274,22 @@ class MHPCLocomotion:
                    "mhpc_get_counters")
         return {k: getattr(c, k) for k, _ in capi.Counters._fields_}
 
+    def set_profiling(self, on: bool = True):
+        capi.check(capi.lib().mhpc_set_profiling(self._h, 1 if on else 0), "mhpc_set_profiling")
+
+    def kernel_stats(self) -> dict:
+        n = capi.MHPC_NUM_KERNELS
+        ms, nl, by = np.zeros(n), np.zeros(n, dtype=np.int64), np.zeros(n)
+        capi.check(capi.lib().mhpc_get_kernel_stats(
+            self._h, capi.dptr(ms), nl.ctypes.data_as(__import__("ctypes").POINTER(
+                __import__("ctypes").c_int64)), capi.dptr(by)), "mhpc_get_kernel_stats")
+        return {capi.lib().mhpc_kernel_name(k).decode(): {"ms": float(ms[k]), "launches": int(nl[k]),
+                                                          "alg_bytes": float(by[k])}
+                for k in range(n)}
+
+    def reset_kernel_stats(self):
+        capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
+
     def concatenated(self) -> dict:
         """Phase-concatenated per-problem arrays (the oracle's layout)."""
         parts = [self.get_phase(p) for p in range(self.desc.n_phases)]
