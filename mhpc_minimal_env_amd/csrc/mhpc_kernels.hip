@@ -20,147 +20,9 @@
 //   k_al_end   AL / ReB parameter update and outer-loop exit (MultiPhaseDDP.cpp:273-284).
 #include <hip/hip_runtime.h>
 
-#include "mhpc_model.h"
-#include "mhpc_solver.h"
+#include "mhpc_device.h"
 
 namespace mhpc {
-
-constexpr double PI = 3.141592653589793238;  // MHPC_CPPTypes.h:18
-
-// ---- cost weights (MHPCCost.cpp:24-75) ------------------------------------------------
-__constant__ double cQwb[14] = {0.01 * 0, 0.01 * 10, 0.01 * 5, 0.01 * 4, 0.01 * 4, 0.01 * 4,
-                                0.01 * 4, 0.01 * 2, 0.01 * 1, 0.01 * .01, 0.01 * 6, 0.01 * 6,
-                                0.01 * 6, 0.01 * 6};
-__constant__ double cQfwb[4][14] = {
-    {100 * 0., 100 * 20., 100 * 8., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 2.,
-     100 * 0.01, 100 * 5., 100 * 5., 100 * 0.01, 100 * 0.01},
-    {100 * 0., 100 * 20., 100 * 8., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 2.,
-     100 * 0.01, 100 * 5., 100 * 5., 100 * 5., 100 * 5.},
-    {100 * 0., 100 * 20., 100 * 8., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 2.,
-     100 * 0.01, 100 * 0.01, 100 * 0.01, 100 * 5., 100 * 5.},
-    {100 * 0., 100 * 20., 100 * 8., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 3., 100 * 2.,
-     100 * 0.01, 100 * 5., 100 * 5., 100 * 5., 100 * 5.}};
-__constant__ double cRwb[4][4] = {{0.5 * 5, 0.5 * 5, 0.5 * 1, 0.5 * 1},
-                                  {0.5 * 1, 0.5 * 1, 0.5 * 1, 0.5 * 1},
-                                  {0.5 * 1, 0.5 * 1, 0.5 * 5, 0.5 * 5},
-                                  {0.5 * 1, 0.5 * 1, 0.5 * 1, 0.5 * 1}};
-// s[3] is uninitialised in the reference (MHPCCost.cpp:43 fills s[0..2]); zero here, as in
-// the oracle.  It can only offset the value of WB mode-4 running costs (y = 0 in flight).
-__constant__ double cSwb[4][4] = {{0, 0, 0.3, 0.3}, {0, 0, 0, 0}, {0.15, 0.15, 0, 0}, {0, 0, 0, 0}};
-__constant__ double cQfb[6] = {0.01 * 0, 0.01 * 10, 0.01 * 5, 0.01 * 2, 0.01 * 1, 0.01 * 0.01};
-__constant__ double cQffb[6] = {100 * 1., 100 * 20., 100 * 8., 100 * 3., 100 * 1., 100 * 0.01};
-__constant__ double cRfb[4][4] = {{0, 0, 0.01, 0.01}, {0, 0, 0, 0}, {0.01, 0.01, 0, 0}, {0, 0, 0, 0}};
-// terminal WB state references (ReferenceGen.cpp:45-52), velocity entry filled at run time
-__constant__ double cXtermWB[4][14] = {
-    {0, -0.1432, -PI / 25, 0.35 * PI, -0.65 * PI, 0.35 * PI, -0.6 * PI, 0, 1, 0, 0, 0, 0, 0},
-    {0, -0.1418, PI / 35, 0.2 * PI, -0.58 * PI, 0.25 * PI, -0.7 * PI, 0, -1, 0, 0, 0, 0, 0},
-    {0, -0.1325, -PI / 40, 0.33 * PI, -0.48 * PI, 0.33 * PI, -0.75 * PI, 0, 1, 0, 0, 0, 0, 0},
-    {0, -0.1490, -PI / 25, 0.35 * PI, -0.7 * PI, 0.25 * PI, -0.60 * PI, 0, -1, 0, 0, 0, 0, 0}};
-__constant__ double cQjointBias[4] = {0.3 * PI, -0.7 * PI, 0.3 * PI, -0.7 * PI};
-constexpr double kGRF = 8.252 * 9.81;  // ReferenceGen.cpp:27
-
-__device__ __forceinline__ double* traj_ptr(const SolveParams& sp, const DevBufs& d, int b,
-                                            int slot, int kk) {
-  return d.traj + (((size_t)b * sp.nslot + slot) * sp.NK + kk) * KS;
-}
-
-__device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (mode == 2 || mode == 4); }
-
-// ---- reduced barrier (SinglePhase.cpp:298-317), k = 2 ---------------------------------
-__device__ __forceinline__ void reduced_barrier(double g, double delta, double* B, double* Bz,
-                                                double* Bzz) {
-  if (g > delta) {
-    *B = -log(g);
-    *Bz = -1.0 / g;
-    *Bzz = pow(g, -2.0);
-  } else {
-    const double t = (g - 2 * delta) / ((2 - 1) * delta);
-    *B = (double)(2 - 1) / 2 * (pow(t, 2.0) - 1) - log(delta);
-    *Bz = pow(t, 1.0) / delta;
-    *Bzz = pow(t, 0.0);
-  }
-}
-
-// Running cost value incl. the ReB barrier of WB phases (CostBase.cpp:4-16,
-// SinglePhase.cpp:219-249 in CALC_DYNAMICS_ONLY), reference of knot kk built in registers.
-__device__ double wb_running_cost(const SolveParams& sp, int mode, double dt, double pos,
-                                  const double* x, const double* u, const double* y, bool reb,
-                                  double delta, double eps_tq, double eps_grf) {
-  const int m = mode - 1;
-  double rx[14] = {pos, sp.height, 0, cQjointBias[0], cQjointBias[1], cQjointBias[2],
-                   cQjointBias[3], sp.vel, 0, 0, 0, 0, 0, 0};
-  const double ry[4] = {0, kGRF, 0, kGRF};
-  double l = 0, t = 0;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) { const double e = x[i] - rx[i]; l += e * cQwb[i] * e; }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { const double e = u[i]; t += e * cRwb[m][i] * e; }
-  l += t;
-  t = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { const double e = y[i] - ry[i]; t += e * cSwb[m][i] * e; }
-  l += t;
-  l = l * dt;
-  if (reb) {
-    double B, Bz, Bzz;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {  // torque limits 33 -/+ u
-      const double g = (i < 4 ? -u[i] : u[i - 4]) + 33;
-      reduced_barrier(g, delta, &B, &Bz, &Bzz);
-      l += eps_tq * B * dt;
-    }
-    // joint limits carry eps_ReB = 0 (MHPCConstraints.cpp:64-84): contribution 0 * B * dt
-    if (mode == 1 || mode == 3) {  // GRF: Fz >= 0, mu Fz -/+ Fx >= 0 with mu = 0.5
-      const int o = mode == 1 ? 2 : 0;
-      const double gs[3] = {y[o + 1], -y[o] + 0.5 * y[o + 1], y[o] + 0.5 * y[o + 1]};
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        reduced_barrier(gs[i], delta, &B, &Bz, &Bzz);
-        l += eps_grf * B * dt;
-      }
-    }
-  }
-  return l;
-}
-
-__device__ double fb_running_cost(const SolveParams& sp, int mode, double dt, double pos,
-                                  const double* x, const double* u) {
-  const int m = mode - 1;
-  const double rx[6] = {pos, sp.height, 0, sp.vel, 0, 0};
-  const double ru[4] = {0, kGRF, 0, kGRF};
-  double l = 0, t = 0;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) { const double e = x[i] - rx[i]; l += e * cQfb[i] * e; }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { const double e = u[i] - ru[i]; t += e * cRfb[m][i] * e; }
-  l += t;
-  l += 0.0;  // S = 0 for the floating base (y = 0)
-  return l * dt;
-}
-
-__device__ void wb_term_ref(const SolveParams& sp, int mode, double pos, double* rx) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) rx[i] = cXtermWB[mode - 1][i];
-  rx[7] = sp.vel;
-  rx[0] = pos;
-}
-
-__device__ void fb_term_ref(const SolveParams& sp, double pos, double* rx) {
-  rx[0] = pos; rx[1] = sp.height; rx[2] = 0; rx[3] = sp.vel; rx[4] = 0; rx[5] = 0;
-}
-
-// FootholdPlanner::get_foothold_location (FootholdPlan.h:26-50), velcmd 1.5 / ground
-// -0.404 hard-coded by the reference (MHPCLocomotion.cpp:25).
-__device__ void plan_foothold(const double* x0, double stance_time, int mode, double* f) {
-  f[0] = f[1] = f[2] = f[3] = 0;
-  if (mode == 1) {
-    f[2] = (cos(x0[2]) * (-0.19) + x0[0]) + 1.5 * stance_time / 2;
-    f[3] = -0.404;
-  } else if (mode == 3) {
-    f[0] = (cos(x0[2]) * 0.19 + x0[0]) + 1.5 * stance_time / 2;
-    f[1] = -0.404;
-  }
-}
 
 // ============================================================================================
 // k_rollout
@@ -242,7 +104,7 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
         for (int i = 0; i < 14; ++i) { const double e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
         Phi = Phi * 0.5;
         if (ntc_of(mode, true)) {
-          h = wb_touchdown_value(x, mode == 2 ? kFront : kBack);
+          h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
           if (sp.AL_active) {
             const double s = st->sigma[p], lam = st->lambda[p];
             Phi += 50 * (pow(s * h / 2, 2.0) + lam * h);
@@ -369,12 +231,21 @@ __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = Dual(nk[14 + i], 14 + i == dir ? 1.0 : 0.0);
     wb_dynamics<Dual>(x, u, mode, f, y);
-    double* out = d.par + ((size_t)b * sp.NK + ko + k) * PS + dir * 9;
+    double* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+    double* out = rec + dir * 9;
 #pragma unroll
     for (int i = 0; i < 7; ++i) out[i] = f[7 + i].d;
-    const int o = mode == 1 ? 2 : 0;
-    out[7] = y[o].d;
-    out[8] = y[o + 1].d;
+    out[7] = mode == 1 ? y[2].d : y[0].d;
+    out[8] = mode == 1 ? y[3].d : y[1].d;
+    if (dir == 0) {
+      // running-cost derivatives of controls and contact forces at the nominal knot
+      // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
+      double c[14];
+      wb_cost_uy_derivs(mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
+                        st->eps_tq[p], st->eps_grf[p], c);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
+    }
   } else {
     const int dir = loc - (N - 1) * 18;
     const double* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
@@ -385,602 +256,6 @@ __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
     double* out = d.px + ((size_t)b * MAXP + p) * 196 + dir * 14;
 #pragma unroll
     for (int i = 0; i < 14; ++i) out[i] = xp[i].d;
-  }
-}
-
-// ============================================================================================
-// k_bws: one wavefront per problem
-// ============================================================================================
-struct BwsLds {
-  double H[196], G[14];            // value function of knot k+1, then of knot k
-  double A[196], Bm[56], C[56], D[16];
-  double lx[14], lxx[14], luu[16], lyy[16];
-  double T[196], BtH[56], Ctl[56], Dtl[16];
-  double Qx[14], Qu[4], Qxx[196], Quu[16], Qux[56];
-  double tq[56];                   // Qux' * Quu_inv   (n x 4)
-  double xb[14], ub[4], yb[4];     // nominal knot
-  double P[PS];                    // partials record of the knot
-  double Px[196];
-  double G2[14], H2[196];          // impact-aware step scratch
-};
-
-// Eigen-style 4x4 inverse by cofactors (same formulas as the oracle).
-__device__ void inverse4(const double* m, double* inv) {
-  double a[16];
-  a[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] +
-         m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
-  a[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] -
-         m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
-  a[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] +
-         m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
-  a[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] -
-          m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
-  a[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] -
-         m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
-  a[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] +
-         m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
-  a[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] -
-         m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
-  a[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] +
-          m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
-  a[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] +
-         m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
-  a[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] -
-         m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
-  a[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] +
-          m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
-  a[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] -
-          m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
-  a[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] -
-         m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
-  a[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] +
-         m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
-  a[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] -
-          m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
-  a[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] +
-          m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
-  const double det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) inv[i] = a[i] / det;
-}
-
-// Eigen LDLT(...).isPositive() on the lower triangle of a 4x4 (see oracle).
-__device__ bool ldlt_is_positive4(const double* Ain) {
-  double A[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) A[i] = Ain[i];
-  int sign = 0;  // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
-  double temp[4];
-  for (int k = 0; k < 4; ++k) {
-    int big = k;
-    double bigv = fabs(A[k * 4 + k]);
-    for (int i = k + 1; i < 4; ++i)
-      if (fabs(A[i * 4 + i]) > bigv) { bigv = fabs(A[i * 4 + i]); big = i; }
-    if (big != k) {
-      for (int jj = 0; jj < k; ++jj) { const double t = A[k * 4 + jj]; A[k * 4 + jj] = A[big * 4 + jj]; A[big * 4 + jj] = t; }
-      for (int i = big + 1; i < 4; ++i) { const double t = A[i * 4 + k]; A[i * 4 + k] = A[i * 4 + big]; A[i * 4 + big] = t; }
-      { const double t = A[k * 4 + k]; A[k * 4 + k] = A[big * 4 + big]; A[big * 4 + big] = t; }
-      for (int i = k + 1; i < big; ++i) { const double t = A[i * 4 + k]; A[i * 4 + k] = A[big * 4 + i]; A[big * 4 + i] = t; }
-    }
-    if (k > 0) {
-      for (int jj = 0; jj < k; ++jj) temp[jj] = A[jj * 4 + jj] * A[k * 4 + jj];
-      double s = 0;
-      for (int jj = 0; jj < k; ++jj) s += A[k * 4 + jj] * temp[jj];
-      A[k * 4 + k] -= s;
-      for (int i = k + 1; i < 4; ++i) {
-        double t = 0;
-        for (int jj = 0; jj < k; ++jj) t += A[i * 4 + jj] * temp[jj];
-        A[i * 4 + k] -= t;
-      }
-    }
-    const double akk = A[k * 4 + k];
-    const bool valid = fabs(akk) > 0.0;
-    if (k == 0 && !valid) { sign = 0; break; }
-    if (k < 3 && valid)
-      for (int i = k + 1; i < 4; ++i) A[i * 4 + k] /= akk;
-    if (sign == 1) { if (akk < 0.0) sign = 3; }
-    else if (sign == 2) { if (akk > 0.0) sign = 3; }
-    else if (sign == 0) { if (akk > 0.0) sign = 1; else if (akk < 0.0) sign = 2; }
-  }
-  return sign == 1 || sign == 0;
-}
-
-// Per-knot cost derivatives, identical for every lane (registers): lu, ly, luu(diag), lyy.
-// lx / lxx per state index are produced by the caller's lanes.  CostBase.cpp:19-34 +
-// SinglePhase.cpp:219-249 (CALC_PARTIALS_ONLY / DYN_AND_PAR branch).
-__device__ void wb_cost_uy(int mode, double dt, const double* u, const double* y, bool reb,
-                           double delta, double eps_tq, double eps_grf, double* lu, double* ly,
-                           double* luu, double* lyy) {
-  const int m = mode - 1;
-  const double c = 2 * dt;
-  const double ry[4] = {0, kGRF, 0, kGRF};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    lu[i] = (c * cRwb[m][i]) * (u[i] - 0.0);
-    ly[i] = (c * cSwb[m][i]) * (y[i] - ry[i]);
-    luu[i] = c * cRwb[m][i];
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) lyy[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) lyy[i * 5] = c * cSwb[m][i];
-  if (!reb) return;
-  double B, Bz, Bzz;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int a = i & 3;
-    const double gu = i < 4 ? -1.0 : 1.0;
-    const double g = gu * u[a] + 33;
-    reduced_barrier(g, delta, &B, &Bz, &Bzz);
-    lu[a] += eps_tq * Bz * gu * dt;
-    luu[a] += eps_tq * (gu * Bzz * gu) * dt;
-  }
-  if (mode == 1 || mode == 3) {
-    const int o = mode == 1 ? 2 : 0;
-    const double rows[3][2] = {{0, 1}, {-1, 0.5}, {1, 0.5}};  // coefficients on (Fx, Fz)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const double g = rows[i][0] * y[o] + rows[i][1] * y[o + 1] + 0;
-      reduced_barrier(g, delta, &B, &Bz, &Bzz);
-#pragma unroll
-      for (int a = 0; a < 2; ++a) ly[o + a] += eps_grf * Bz * rows[i][a] * dt;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2)
-          lyy[(o + a) * 4 + o + c2] += eps_grf * (rows[i][a] * Bzz * rows[i][c2]) * dt;
-    }
-  }
-}
-
-// One backward Riccati knot with NX states (compute_Qfunction + regularisation + PSD test
-// + valuefunction_update).  sh.{A,Bm,C,D,lxx,luu,lyy} and lane-private lx_l/lu/ly hold the
-// knot's derivatives (lx in sh.lx); sh.H/G hold the value function of knot k+1 and
-// receive that of k.
-template <int NX, bool HAS_Y>
-__device__ bool riccati_knot(BwsLds& sh, int lane, const double* lu,
-                             const double* ly, double reg, double eps9, double* Kout,
-                             double* duout, double* Gout, double* dV) {
-  constexpr int N2 = NX * NX, N4 = 4 * NX;
-  // R2: T = A'H, BtH = B'H, Ctl = C'lyy, Dtl = D'lyy, Qx, Qu
-  for (int e = lane; e < N2 + N4 + N4 + 16 + NX + 4; e += 64) {
-    if (e < N2) {
-      const int i = e / NX, jj = e - i * NX;
-      double s = 0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s += sh.A[m * NX + i] * sh.H[m * NX + jj];
-      sh.T[e] = s;
-    } else if (e < N2 + N4) {
-      const int q = e - N2, c = q / NX, jj = q - c * NX;
-      double s = 0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s += sh.Bm[m * 4 + c] * sh.H[m * NX + jj];
-      sh.BtH[q] = s;
-    } else if (e < N2 + 2 * N4) {
-      const int q = e - N2 - N4, i = q / 4, c = q - i * 4;
-      double s = 0;
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += sh.C[r * NX + i] * sh.lyy[r * 4 + c];
-      }
-      sh.Ctl[q] = s;
-    } else if (e < N2 + 2 * N4 + 16) {
-      const int q = e - N2 - 2 * N4, c = q / 4, c2 = q - c * 4;
-      double s = 0;
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += sh.D[r * 4 + c] * sh.lyy[r * 4 + c2];
-      }
-      sh.Dtl[q] = s;
-    } else if (e < N2 + 2 * N4 + 16 + NX) {
-      const int i = e - (N2 + 2 * N4 + 16);
-      double s = 0, s2 = 0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s += sh.A[m * NX + i] * sh.G[m];
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s2 += sh.C[r * NX + i] * ly[r];
-      }
-      sh.Qx[i] = (sh.lx[i] + s) + s2;
-    } else {
-      const int c = e - (N2 + 2 * N4 + 16 + NX);
-      double s = 0, s2 = 0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s += sh.Bm[m * 4 + c] * sh.G[m];
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s2 += sh.D[r * 4 + c] * ly[r];
-      }
-      sh.Qu[c] = (lu[c] + s) + s2;
-    }
-  }
-  __syncthreads();
-  // R3: Qxx = (lxx + Ctl C) + T A ; Quu = (luu + Dtl D) + BtH B ; Qux = Dtl C + BtH A
-  for (int e = lane; e < N2 + 16 + N4; e += 64) {
-    if (e < N2) {
-      const int i = e / NX, jj = e - i * NX;
-      double s = 0, s2 = 0;
-      if (HAS_Y) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s += sh.Ctl[i * 4 + c] * sh.C[c * NX + jj];
-      }
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s2 += sh.T[i * NX + m] * sh.A[m * NX + jj];
-      double v = ((i == jj ? sh.lxx[i] : 0.0) + s) + s2;
-      if (i == jj) v += 1.0 * reg;
-      sh.Qxx[e] = v;
-    } else if (e < N2 + 16) {
-      const int q = e - N2, c = q / 4, c2 = q - c * 4;
-      double s = 0, s2 = 0;
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += sh.Dtl[c * 4 + r] * sh.D[r * 4 + c2];
-      }
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s2 += sh.BtH[c * NX + m] * sh.Bm[m * 4 + c2];
-      double v = (sh.luu[q] + s) + s2;
-      if (c == c2) v += 1.0 * reg;
-      sh.Quu[q] = v;
-    } else {
-      const int q = e - N2 - 16, c = q / NX, jj = q - c * NX;
-      double s = 0, s2 = 0;
-      if (HAS_Y) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += sh.Dtl[c * 4 + r] * sh.C[r * NX + jj];
-      }
-#pragma unroll
-      for (int m = 0; m < NX; ++m) s2 += sh.BtH[c * NX + m] * sh.A[m * NX + jj];
-      sh.Qux[q] = (0.0 + s) + s2;
-    }
-  }
-  __syncthreads();
-  // R4 (all lanes, registers): PSD test of Quu - 1e-9 I, inverse, du, dV
-  double Quu[16], Qr[16], inv[16], Qi[16], Qu[4];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { Quu[i] = sh.Quu[i]; Qr[i] = Quu[i] - ((i % 5 == 0) ? 1.0 * eps9 : 0.0); }
-  if (!ldlt_is_positive4(Qr)) return false;
-  inverse4(Quu, inv);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) Qi[i * 4 + c] = (inv[i * 4 + c] + inv[c * 4 + i]) / 2;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) Qu[i] = sh.Qu[i];
-  {
-    double r[4], s = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double t = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t += Qu[k] * inv[k * 4 + c];
-      r[c] = t;
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s += r[c] * Qu[c];
-    *dV += -s;
-  }
-  if (lane < 4) {
-    double s = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s += -Qi[lane * 4 + c] * Qu[c];
-    duout[lane] = s;
-  }
-  // K = -Quu_inv Qux (4 x NX) and tq = Qux' Quu_inv (NX x 4)
-  for (int e = lane; e < 2 * N4; e += 64) {
-    if (e < N4) {
-      const int c = e / NX, jj = e - c * NX;
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += -Qi[c * 4 + k] * sh.Qux[k * NX + jj];
-      Kout[e] = s;
-    } else {
-      const int q = e - N4, i = q / 4, c = q - i * 4;
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += sh.Qux[k * NX + i] * Qi[k * 4 + c];
-      sh.tq[q] = s;
-    }
-  }
-  __syncthreads();
-  // R5: H = sym(Qxx) - tq Qux ; G = Qx - tq Qu
-  for (int e = lane; e < N2 + NX; e += 64) {
-    if (e < N2) {
-      const int i = e / NX, jj = e - i * NX;
-      double s = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += sh.tq[i * 4 + c] * sh.Qux[c * NX + jj];
-      sh.H[e] = (sh.Qxx[e] + sh.Qxx[jj * NX + i]) / 2 - s;
-    } else {
-      const int i = e - N2;
-      double s = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += sh.tq[i * 4 + c] * Qu[c];
-      const double g = sh.Qx[i] - s;
-      sh.G[i] = g;
-      Gout[i] = g;
-    }
-  }
-  __syncthreads();
-  return true;
-}
-
-// Terminal value function of phase p at its last knot (SinglePhase.cpp:189-191):
-// G = Phix + Gnext, H = Phixx + Hnext with Gnext/Hnext in sh.G/sh.H on entry.
-template <int NX>
-__device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLds& sh, int lane,
-                               int p, bool wb, double pos, const double* xe, double* Gout) {
-  const int mode = sp.mode[p];
-  double rx[14];
-  if (wb) wb_term_ref(sp, mode, pos, rx);
-  else fb_term_ref(sp, pos, rx);
-  const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
-  double h = 0, hx[14], Hs[3][3];
-  int id[3] = {0, 0, 0};
-  if (al) wb_touchdown_compact(xe, mode == 2 ? kFront : kBack, &h, hx, id, Hs);
-  const double s = st->sigma[p], lam = st->lambda[p];
-  for (int e = lane; e < NX * NX + NX; e += 64) {
-    if (e < NX * NX) {
-      const int i = e / NX, jj = e - i * NX;
-      double v = i == jj ? (wb ? cQfwb[mode - 1][i] : cQffb[i]) : 0.0;
-      if (al) {
-        double hij = 0;
-        for (int a = 0; a < 3; ++a)
-          for (int c = 0; c < 3; ++c)
-            if (id[a] == i && id[c] == jj) hij = Hs[a][c];
-        v += 50 * (s * s / 2 * (hx[i] * hx[jj] + h * hij) + lam * hij);
-      }
-      sh.H[e] = v + sh.H[e];
-    } else {
-      const int i = e - NX * NX;
-      double v = (wb ? cQfwb[mode - 1][i] : cQffb[i]) * (xe[i] - rx[i]);
-      if (al) v += 50 * (s * s / 2 * hx[i] * h + lam * hx[i]);
-      const double g = v + sh.G[i];
-      sh.G[i] = g;
-      Gout[i] = g;
-    }
-  }
-  __syncthreads();
-}
-
-__device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st,
-                          BwsLds& sh, double reg, int64_t* knots, int64_t* knots_wb,
-                          int64_t* px_reads) {
-  const int lane = threadIdx.x;
-  const int nom = st->nom_slot;
-  double dVnext = 0;
-  // Gnext = 0, Hnext = 0 for the last phase
-  for (int e = lane; e < 196; e += 64) sh.H[e] = 0;
-  if (lane < 14) sh.G[lane] = 0;
-  __syncthreads();
-  for (int p = sp.P - 1; p >= 0; --p) {
-    const bool wb = p < sp.n_wb;
-    const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-    const double dt = sp.dt[p];
-    if (p + 1 < sp.P) {
-      // impact_aware_step (MultiPhaseDDP.cpp:300-341); sh.G/H hold CTG[0] of phase p+1
-      dVnext = st->dV[p + 1];
-      if (wb) {
-        const bool nwb = p + 1 < sp.n_wb;
-        const bool imp = mode == 2 || mode == 4;
-        if (imp) {
-          const double* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
-          for (int e = lane; e < 196; e += 64) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
-          ++*px_reads;
-        } else {
-          for (int e = lane; e < 196; e += 64) sh.Px[e] = (e / 14 == e % 14) ? 1.0 : 0.0;
-        }
-        // lift G', H' of the next phase to the 14-dim full-model space: E' G', E' H' E
-        // (E = _stateProj for an SRB next phase, identity otherwise)
-        __syncthreads();
-        for (int e = lane; e < 196 + 14; e += 64) {
-          if (e < 196) {
-            const int i = e / 14, jj = e % 14;
-            double v = 0;
-            if (nwb) v = sh.H[e];
-            else {
-              int pi = -1, pj = -1;
-              for (int q = 0; q < 6; ++q) {
-                const int r = q < 3 ? q : q + 4;
-                if (r == i) pi = q;
-                if (r == jj) pj = q;
-              }
-              v = (pi >= 0 && pj >= 0) ? sh.H[pi * 6 + pj] : 0.0;
-            }
-            sh.H2[e] = v;
-          } else {
-            const int i = e - 196;
-            double v = 0;
-            if (nwb) v = sh.G[i];
-            else {
-              const int q = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
-              v = q >= 0 ? sh.G[q] : 0.0;
-            }
-            sh.G2[i] = v;
-          }
-        }
-        __syncthreads();
-        if (imp) {
-          // G = Px' G2 ; T = Px' H2 ; H = T Px
-          for (int e = lane; e < 196 + 14; e += 64) {
-            if (e < 196) {
-              const int i = e / 14, jj = e % 14;
-              double s = 0;
-              for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.H2[m * 14 + jj];
-              sh.T[e] = s;
-            } else {
-              const int i = e - 196;
-              double s = 0;
-              for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.G2[m];
-              sh.G[i] = s;
-            }
-          }
-          __syncthreads();
-          for (int e = lane; e < 196; e += 64) {
-            const int i = e / 14, jj = e % 14;
-            double s = 0;
-            for (int m = 0; m < 14; ++m) s += sh.T[i * 14 + m] * sh.Px[m * 14 + jj];
-            sh.H[e] = s;
-          }
-        } else {
-          for (int e = lane; e < 196; e += 64) sh.H[e] = sh.H2[e];
-          if (lane < 14) sh.G[lane] = sh.G2[lane];
-        }
-        __syncthreads();
-      }
-      // SRB current phase: G = G', H = H' (already in place)
-    }
-    double dV = dVnext;
-    const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-    double* Gp = d.G + ((size_t)b * sp.NK + ko) * 14;
-    const double* xe = traj_ptr(sp, d, b, nom, ko + N - 1);
-    if (wb) terminal_value<14>(sp, st, sh, lane, p, true, pos[N - 1], xe, Gp + (size_t)(N - 1) * 14);
-    else terminal_value<6>(sp, st, sh, lane, p, false, pos[N - 1], xe, Gp + (size_t)(N - 1) * 14);
-    double foot[4] = {0, 0, 0, 0}, cs[2] = {0, 0};
-    if (!wb) {
-      plan_foothold(traj_ptr(sp, d, b, nom, ko), dt * N, mode, foot);
-      srb_contact(mode, cs);
-    }
-    const bool reb = st->reb_active;
-    const double delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
-    for (int k = N - 2; k >= 0; --k) {
-      const int kk = ko + k;
-      const double* nk = traj_ptr(sp, d, b, nom, kk);
-      double* Kout = d.K + ((size_t)b * sp.NK + kk) * 56;
-      double* duout = d.du + ((size_t)b * sp.NK + kk) * 4;
-      double* Gout = d.G + ((size_t)b * sp.NK + kk) * 14;
-      bool ok;
-      if (wb) {
-        const double* prec = d.par + ((size_t)b * sp.NK + kk) * PS;
-        for (int e = lane; e < PS; e += 64) sh.P[e] = prec[e];
-        if (lane < 22) {
-          const double v = nk[lane];
-          if (lane < 14) sh.xb[lane] = v;
-          else if (lane < 18) sh.ub[lane - 14] = v;
-          else sh.yb[lane - 18] = v;
-        }
-        __syncthreads();
-        // A = I + dt Ac, B = dt Bc, C, D (PlanarQuadruped.cpp:51-52)
-        const int o = mode == 1 ? 2 : 0;
-        const bool stance = mode == 1 || mode == 3;
-        for (int e = lane; e < 196 + 56 + 56 + 16; e += 64) {
-          if (e < 196) {
-            const int i = e / 14, jj = e % 14;
-            const double ac = i < 7 ? (jj == i + 7 ? 1.0 : 0.0) : sh.P[jj * 9 + (i - 7)];
-            sh.A[e] = (i == jj ? 1.0 : 0.0) + ac * dt;
-          } else if (e < 252) {
-            const int q = e - 196, i = q / 4, c = q % 4;
-            sh.Bm[q] = (i < 7 ? 0.0 : sh.P[(14 + c) * 9 + (i - 7)]) * dt;
-          } else if (e < 308) {
-            const int q = e - 252, r = q / 14, jj = q % 14;
-            sh.C[q] = (stance && (r == o || r == o + 1)) ? sh.P[jj * 9 + 7 + (r - o)] : 0.0;
-          } else {
-            const int q = e - 308, r = q / 4, c = q % 4;
-            sh.D[q] = (stance && (r == o || r == o + 1)) ? sh.P[(14 + c) * 9 + 7 + (r - o)] : 0.0;
-          }
-        }
-        double lu[4], ly[4], luu[4], lyy[16];
-        wb_cost_uy(mode, dt, sh.ub, sh.yb, reb, delta, etq, egr, lu, ly, luu, lyy);
-        // lx, lxx (CostBase.cpp:28-31) for state index = lane
-        double lx_l = 0;
-        {
-          const int i = lane < 14 ? lane : 0;
-          const double rxi = i == 0 ? pos[k] : i == 1 ? sp.height : i == 2 ? 0.0
-                             : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : 0.0;
-          lx_l = (2 * dt * cQwb[i]) * (sh.xb[i] - rxi);
-          if (lane < 14) sh.lxx[lane] = 2 * dt * cQwb[lane];
-        }
-        if (lane < 16) {
-          sh.luu[lane] = (lane % 5 == 0) ? luu[lane / 5] : 0.0;
-          sh.lyy[lane] = lyy[lane];
-        }
-        if (lane < 14) sh.lx[lane] = lx_l;
-        __syncthreads();
-        ok = riccati_knot<14, true>(sh, lane, lu, ly, reg, sp.eps9, Kout, duout, Gout, &dV);
-      } else {
-        if (lane < 10) {
-          const double v = nk[lane];
-          if (lane < 6) sh.xb[lane] = v;
-          else sh.ub[lane - 6] = v;
-        }
-        __syncthreads();
-        double Ac[36], Bc[24];
-        srb_jacobians(sh.xb, sh.ub, foot, cs, Ac, Bc);
-        for (int e = lane; e < 36 + 24; e += 64) {
-          if (e < 36) sh.A[e] = ((e / 6 == e % 6) ? 1.0 : 0.0) + Ac[e] * dt;
-          else sh.Bm[e - 36] = Bc[e - 36] * dt;
-        }
-        const int m = mode - 1;
-        double lu[4], ly[4] = {0, 0, 0, 0};
-        const double ru[4] = {0, kGRF, 0, kGRF};
-        for (int c = 0; c < 4; ++c) lu[c] = (2 * dt * cRfb[m][c]) * (sh.ub[c] - ru[c]);
-        double lx_l = 0;
-        {
-          const int i = lane < 6 ? lane : 0;
-          const double rxi = i == 0 ? pos[k] : i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
-          lx_l = (2 * dt * cQfb[i]) * (sh.xb[i] - rxi);
-          if (lane < 6) sh.lxx[lane] = 2 * dt * cQfb[lane];
-        }
-        if (lane < 16) {
-          sh.luu[lane] = (lane % 5 == 0) ? 2 * dt * cRfb[m][lane / 5] : 0.0;
-          sh.lyy[lane] = 0;
-        }
-        if (lane < 6) sh.lx[lane] = lx_l;
-        __syncthreads();
-        ok = riccati_knot<6, false>(sh, lane, lu, ly, reg, sp.eps9, Kout, duout, Gout, &dV);
-      }
-      ++*knots;
-      if (wb) ++*knots_wb;
-      if (!ok) {
-        st->dV[p] = dV;
-        return false;
-      }
-    }
-    st->dV[p] = dV;
-  }
-  return true;
-}
-
-__global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
-  const int b = blockIdx.x;
-  if (b >= sp.B) return;
-  ProbState* st = &d.st[b];
-  if (!(st->active && st->ddp_active)) return;
-  __shared__ BwsLds sh;
-  double reg = st->reg;
-  int bws_iter = 1;
-  int64_t knots = 0, knots_wb = 0, px_reads = 0;
-  int64_t sweeps = 0;
-  bool aborted = false;
-  for (;;) {
-    ++sweeps;
-    const bool ok = bws_sweep(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
-    if (ok) break;
-    reg = fmax(reg * update_reg, 1e-03);
-    ++bws_iter;
-    if (reg > 1000) { aborted = true; break; }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    st->cnt[C_DDP]++;
-    st->cnt[C_BWS] += sweeps;
-    st->cnt[C_BWS_KNOTS] += knots;
-    st->cnt[C_BWS_KNOTS_WB] += knots_wb;
-    st->cnt[C_BWS_KNOTS_FB] += knots - knots_wb;
-    st->cnt[C_PX_READS] += px_reads;
-    st->bws_iter = bws_iter;
-    if (aborted) {
-      st->status = MHPC_SOLVE_REG_ABORT;
-      st->active = 0;
-      st->ddp_active = 0;
-      if (st->ntrace < TRACE)
-        st->trace[st->ntrace++] = (st->al_iter << 24) | (st->reb_active << 23) | (1 << 21) |
-                                  (bws_iter & 0xff);
-    } else {
-      st->dV_exp = st->dV[0];
-      reg = reg / 20;
-      if (reg < 1e-06) reg = 0;
-      st->reg = reg;
-    }
   }
 }
 
@@ -1049,10 +324,9 @@ __global__ void k_init(SolveParams sp, DevBufs d) {
     for (int k = 0; k < N - 1; ++k) {
       double u[4];
       if (mode == 1 || mode == 3) {
-        const int foot = mode == 1 ? kBack : kFront;
         double J[14], Jd[14], v[2];
-        wb_foot_jacobian(x, foot, J, Jd);
-        wb_leg_ext(x, foot, v);
+        if (mode == 1) { wb_foot_jacobian_f<kBack>(x, J, Jd); wb_leg_ext<kBack>(x, v); }
+        else { wb_foot_jacobian_f<kFront>(x, J, Jd); wb_leg_ext<kFront>(x, v); }
         const double sq = v[0] * v[0] + v[1] * v[1], nrm = sqrt(sq);
         const double n0 = v[0] / nrm, n1 = v[1] / nrm;
         const double F0 = -n0 * 2200.0 * (nrm - 0.2462), F1 = -n1 * 2200.0 * (nrm - 0.2462);
@@ -1164,10 +438,6 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   const long total = (long)sp.B * sp.par_items;
   if (total == 0) return hipSuccess;
   hipLaunchKernelGGL(k_partials, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sp, d);
-  return hipGetLastError();
-}
-hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, double update_reg, hipStream_t s) {
-  hipLaunchKernelGGL(k_bws, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   return hipGetLastError();
 }
 hipError_t launch_al_end(const SolveParams& sp, const DevBufs& d, int last, hipStream_t s) {

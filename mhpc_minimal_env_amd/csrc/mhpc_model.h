@@ -81,13 +81,16 @@ MHPC_HD void wb_geometry(const S* x, WbGeo<S>& g) {
   }
 }
 
-// Jacobian of a point on leg f at distance l1 down the thigh and l2 down the shank,
-// compact over the local columns (x, z, th, hip, knee); plus Jdot*qdot.
-template <class S>
-MHPC_HD void leg_point_jac(const WbGeo<S>& g, int f, double l1, double l2,
-                           S jx[5], S jz[5], S* jdx, S* jdz) {
-  const double sg = f == kFront ? 1.0 : -1.0;
-  const LegGeo<S>& L = g.leg[f];
+// Jacobian of a point on leg F at distance l1 down the thigh and l2 down the shank,
+// compact over the local columns (x, z, th, hip, knee), plus the centripetal part of
+// Jdot*qdot due to the two link rotations (the hip-offset part is added by the caller).
+// The leg index is a template parameter everywhere so that no register array is indexed
+// with a run-time value (which would spill it to scratch memory on the GPU).
+template <class S, int F>
+MHPC_HD void leg_point_jac(const WbGeo<S>& g, double l1, double l2, S jx[5], S jz[5], S* jdx,
+                           S* jdz) {
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  const LegGeo<S>& L = g.leg[F];
   // d/da of l*(-sin a, -cos a) = l*(-cos a, sin a)
   const S tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
   const S tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
@@ -98,7 +101,6 @@ MHPC_HD void leg_point_jac(const WbGeo<S>& g, int f, double l1, double l2,
   jz[3] = tz1 + tz2;
   jx[2] = (-sg * kHipX) * g.sth + jx[3];
   jz[2] = (-sg * kHipX) * g.cth + jz[3];
-  // centripetal terms of the two link offsets (the hip offset is added by the caller)
   *jdx = L.w1 * L.w1 * (l1 * L.s1) + L.w2 * L.w2 * (l2 * L.s2);
   *jdz = L.w1 * L.w1 * (l1 * L.c1) + L.w2 * L.w2 * (l2 * L.c2);
 }
@@ -106,63 +108,77 @@ MHPC_HD void leg_point_jac(const WbGeo<S>& g, int f, double l1, double l2,
 // Packed lower-triangular index of the symmetric 7x7 mass matrix.
 MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
-// M(q) (packed lower triangle, 28 entries) and bias h(q, qdot) = C qdot + g.
-template <class S>
-MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
-  for (int i = 0; i < 7; ++i) h[i] = S(0.0);
-  for (int i = 0; i < 28; ++i) M[i] = S(0.0);
+// Contribution of the thigh and shank of leg F to M (packed) and h.
+template <class S, int F>
+MHPC_HD void add_leg(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
   const S thd2 = x[9] * x[9];
-  M[tri(0, 0)] = S(kBodyMass);
-  M[tri(1, 1)] = S(kBodyMass);
-  M[tri(2, 2)] = S(kBodyInertia);
-  h[1] = S(kBodyMass * kGrav);
-  for (int f = 0; f < 2; ++f) {
-    const double sg = f == kFront ? 1.0 : -1.0;
-    const int idx[5] = {0, 1, 2, 3 + 2 * f, 4 + 2 * f};
-    // centripetal acceleration of the hip point
-    const S hax = (-sg * kHipX) * g.cth * thd2;
-    const S haz = (sg * kHipX) * g.sth * thd2;
-    for (int b = 0; b < 2; ++b) {  // thigh, shank
-      S jx[5], jz[5], jdx, jdz;
-      double m, ic;
-      int nc;
-      if (b == 0) {
-        leg_point_jac(g, f, kThighCom, 0.0, jx, jz, &jdx, &jdz);
-        m = kThighMass; ic = kThighInertiaCom; nc = 4;
-      } else {
-        leg_point_jac(g, f, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
-        m = kShankMass; ic = kShankInertiaCom; nc = 5;
-      }
-      jdx += hax;
-      jdz += haz;
-      const S ax = jdx, az = jdz + kGrav;
-      for (int a = 0; a < nc; ++a) {
-        h[idx[a]] += m * (jx[a] * ax + jz[a] * az);
-        for (int c = 0; c <= a; ++c) {
-          // x/z columns of a CoM Jacobian are unit vectors: skip the exact zeros
-          if (a < 2 && c < 2) {
-            if (a == c) M[tri(idx[a], idx[c])] += S(m);
-            continue;
-          }
-          S v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
-          if (a >= 2 && c >= 2) v += ic;
-          M[tri(idx[a], idx[c])] += v;
+  const S hax = (-sg * kHipX) * g.cth * thd2;  // centripetal acceleration of the hip point
+  const S haz = (sg * kHipX) * g.sth * thd2;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {  // thigh, shank
+    S jx[5], jz[5], jdx, jdz;
+    double m, ic;
+    if (b == 0) {
+      leg_point_jac<S, F>(g, kThighCom, 0.0, jx, jz, &jdx, &jdz);
+      m = kThighMass; ic = kThighInertiaCom;
+    } else {
+      leg_point_jac<S, F>(g, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
+      m = kShankMass; ic = kShankInertiaCom;
+    }
+    const int nc = b == 0 ? 4 : 5;
+    jdx += hax;
+    jdz += haz;
+    const S ax = jdx, az = jdz + kGrav;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      if (a >= nc) continue;
+      h[idx[a]] += m * (jx[a] * ax + jz[a] * az);
+#pragma unroll
+      for (int c = 0; c <= a; ++c) {
+        // x/z columns of a CoM Jacobian are unit vectors: skip the exact zeros
+        if (a < 2 && c < 2) {
+          if (a == c) M[tri(idx[a], idx[c])] += S(m);
+          continue;
         }
+        S v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
+        if (a >= 2 && c >= 2) v += ic;
+        M[tri(idx[a], idx[c])] += v;
       }
     }
   }
 }
 
+// M(q) (packed lower triangle, 28 entries) and bias h(q, qdot) = C qdot + g.
+template <class S>
+MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
+#pragma unroll
+  for (int i = 0; i < 7; ++i) h[i] = S(0.0);
+#pragma unroll
+  for (int i = 0; i < 28; ++i) M[i] = S(0.0);
+  M[tri(0, 0)] = S(kBodyMass);
+  M[tri(1, 1)] = S(kBodyMass);
+  M[tri(2, 2)] = S(kBodyInertia);
+  h[1] = S(kBodyMass * kGrav);
+  add_leg<S, kFront>(x, g, M, h);
+  add_leg<S, kBack>(x, g, M, h);
+}
+
 // In-place Cholesky M = L L' on the packed lower triangle.
 template <class S>
 MHPC_HD void chol7(S A[28]) {
+#pragma unroll
   for (int j = 0; j < 7; ++j) {
     S d = A[tri(j, j)];
+#pragma unroll
     for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
     const S l = sqrt_(d);
     A[tri(j, j)] = l;
+#pragma unroll
     for (int i = j + 1; i < 7; ++i) {
       S s = A[tri(i, j)];
+#pragma unroll
       for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
       A[tri(i, j)] = s / l;
     }
@@ -171,44 +187,52 @@ MHPC_HD void chol7(S A[28]) {
 
 template <class S>
 MHPC_HD void chol7_solve(const S L[28], S b[7]) {
+#pragma unroll
   for (int i = 0; i < 7; ++i) {
     S s = b[i];
+#pragma unroll
     for (int k = 0; k < i; ++k) s -= L[tri(i, k)] * b[k];
     b[i] = s / L[tri(i, i)];
   }
+#pragma unroll
   for (int i = 6; i >= 0; --i) {
     S s = b[i];
+#pragma unroll
     for (int k = i + 1; k < 7; ++k) s -= L[tri(k, i)] * b[k];
     b[i] = s / L[tri(i, i)];
   }
 }
 
-// Foot Jacobian (2x7, dense) and Jdot*qdot of foot f.
-template <class S>
-MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, int f, S J[2][7], S jd[2]) {
+// Foot Jacobian (2x7, dense) and Jdot*qdot of foot F.
+template <class S, int F>
+MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, S J[2][7], S jd[2]) {
   S jx[5], jz[5], jdx, jdz;
-  leg_point_jac(g, f, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
-  const double sg = f == kFront ? 1.0 : -1.0;
+  leg_point_jac<S, F>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
   const S thd2 = x[9] * x[9];
   jd[0] = jdx + (-sg * kHipX) * g.cth * thd2;
   jd[1] = jdz + (sg * kHipX) * g.sth * thd2;
+  constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
+#pragma unroll
   for (int i = 0; i < 7; ++i) { J[0][i] = S(0.0); J[1][i] = S(0.0); }
-  const int idx[5] = {0, 1, 2, 3 + 2 * f, 4 + 2 * f};
+#pragma unroll
   for (int a = 0; a < 5; ++a) { J[0][idx[a]] = jx[a]; J[1][idx[a]] = jz[a]; }
 }
 
 // Schur-complement solve of the contact KKT system
 //   [M -J'; J 0] [v; lam] = [rhs; -c]  ->  v = M^-1 (rhs + J' lam)
-// given the Cholesky factor L of M.
+// given the Cholesky factor L of M; v holds M^-1 rhs on entry.
 template <class S>
 MHPC_HD void kkt_contact(const S L[28], const S J[2][7], const S c[2], S v[7], S lam[2]) {
-  // v currently holds M^-1 rhs
   S Y[2][7];
+#pragma unroll
   for (int r = 0; r < 2; ++r) {
+#pragma unroll
     for (int i = 0; i < 7; ++i) Y[r][i] = J[r][i];
     chol7_solve(L, Y[r]);
   }
   S A00 = S(0.0), A01 = S(0.0), A11 = S(0.0), r0 = -c[0], r1 = -c[1];
+#pragma unroll
   for (int i = 0; i < 7; ++i) {
     A00 += J[0][i] * Y[0][i];
     A01 += J[0][i] * Y[1][i];
@@ -219,7 +243,18 @@ MHPC_HD void kkt_contact(const S L[28], const S J[2][7], const S c[2], S v[7], S
   const S det = A00 * A11 - A01 * A01;
   lam[0] = (A11 * r0 - A01 * r1) / det;
   lam[1] = (A00 * r1 - A01 * r0) / det;
+#pragma unroll
   for (int i = 0; i < 7; ++i) v[i] += Y[0][i] * lam[0] + Y[1][i] * lam[1];
+}
+
+// Stance dynamics with foot F on the ground (Dyn_FS: F = front, Dyn_BS: F = back).
+template <class S, int F>
+MHPC_HD void wb_stance(const S* x, const WbGeo<S>& g, const S L[28], S v[7], S* y) {
+  S J[2][7], jd[2], lam[2];
+  wb_foot_jac_full<S, F>(x, g, J, jd);
+  kkt_contact(L, J, jd, v, lam);
+  y[2 * F] = lam[0];
+  y[2 * F + 1] = lam[1];
 }
 
 // Continuous whole-body dynamics: xdot = (qdot, qddot), y = contact force of the stance
@@ -234,60 +269,66 @@ MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
   chol7(M);
   S v[7];
   v[0] = -h[0]; v[1] = -h[1]; v[2] = -h[2];
+#pragma unroll
   for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
   chol7_solve(M, v);
+#pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = S(0.0);
-  if (mode == 1 || mode == 3) {
-    const int f = mode == 3 ? kFront : kBack;
-    S J[2][7], jd[2], lam[2];
-    wb_foot_jac_full(x, g, f, J, jd);
-    kkt_contact(M, J, jd, v, lam);
-    y[2 * f] = lam[0];
-    y[2 * f + 1] = lam[1];
-  }
+  if (mode == 1) wb_stance<S, kBack>(x, g, M, v, y);
+  else if (mode == 3) wb_stance<S, kFront>(x, g, M, v, y);
+#pragma unroll
   for (int i = 0; i < 7; ++i) {
     xdot[i] = x[7 + i];
     xdot[7 + i] = v[i];
   }
 }
 
-// Plastic impact of foot f (Imp_F: f = front, end of mode 2; Imp_B: back, end of mode 4):
+// Plastic impact of foot F (Imp_F: front, end of mode 2; Imp_B: back, end of mode 4):
 // q+ = q, [M -J'; J 0][qd+; Lam] = [M qd-; 0].
-template <class S>
-MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
+template <class S, int F>
+MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
   WbGeo<S> g;
   wb_geometry(x, g);
   S M[28], h[7];
   wb_mass_bias(x, g, M, h);
   chol7(M);
   S J[2][7], jd[2];
-  wb_foot_jac_full(x, g, f, J, jd);
+  wb_foot_jac_full<S, F>(x, g, J, jd);
   S v[7], c[2];
-  for (int i = 0; i < 7; ++i) v[i] = x[7 + i];   // M^-1 (M qd-) = qd-
-  c[0] = S(0.0); c[1] = S(0.0);
-  // J qd+ = 0  <=>  J v + J Y lam = 0 with rhs -c = 0
-  kkt_contact(M, J, c, v, Lam);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) v[i] = x[7 + i];  // M^-1 (M qd-) = qd-
+  c[0] = S(0.0);
+  c[1] = S(0.0);
+  kkt_contact(M, J, c, v, Lam);  // J qd+ = 0
+#pragma unroll
   for (int i = 0; i < 7; ++i) {
     xp[i] = x[i];
     xp[7 + i] = v[i];
   }
 }
 
-// Touchdown constraint h = foot_z + 0.404 (foot f = front for mode 2 / WB_FL1, back for
+template <class S>
+MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
+  if (f == kFront) wb_impact_f<S, kFront>(x, xp, Lam);
+  else wb_impact_f<S, kBack>(x, xp, Lam);
+}
+
+// Touchdown constraint h = foot_z + 0.404 (foot F = front for mode 2 / WB_FL1, back for
 // mode 4 / WB_FL2) with its gradient hx (14) and the 3x3 non-zero block of its Hessian on
-// the state indices id[] = (theta, hip, knee) of that leg.
-MHPC_HD double wb_touchdown_value(const double* x, int f) {
-  const double sg = f == kFront ? 1.0 : -1.0;
-  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+// the state indices (theta, hip, knee) of that leg.
+template <int F>
+MHPC_HD double wb_touchdown_value(const double* x) {
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   const double a1 = x[2] + x[ih];
   const double a2 = a1 + x[ik];
   return x[1] - sg * kHipX * sin(x[2]) - kThighLen * cos(a1) - kShankLen * cos(a2) - kGroundHeight;
 }
 
-MHPC_HD void wb_touchdown_compact(const double* x, int f, double* h, double* hx, int id[3],
-                                  double Hs[3][3]) {
-  const double sg = f == kFront ? 1.0 : -1.0;
-  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+template <int F>
+MHPC_HD void wb_touchdown_compact(const double* x, double* h, double* hx, double Hs[3][3]) {
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   double sth, cth, s1, c1, s2, c2;
   sin_cos(x[2], &sth, &cth);
   const double a1 = x[2] + x[ih];
@@ -295,6 +336,7 @@ MHPC_HD void wb_touchdown_compact(const double* x, int f, double* h, double* hx,
   sin_cos(a1, &s1, &c1);
   sin_cos(a2, &s2, &c2);
   *h = x[1] - sg * kHipX * sth - kThighLen * c1 - kShankLen * c2 - kGroundHeight;
+#pragma unroll
   for (int i = 0; i < 14; ++i) hx[i] = 0.0;
   const double dk = kShankLen * s2;
   const double dh = kThighLen * s1 + dk;
@@ -305,17 +347,17 @@ MHPC_HD void wb_touchdown_compact(const double* x, int f, double* h, double* hx,
   const double ek = kShankLen * c2;
   const double eh = kThighLen * c1 + ek;
   const double et = sg * kHipX * sth + eh;
-  id[0] = 2; id[1] = ih; id[2] = ik;
   Hs[0][0] = et; Hs[0][1] = eh; Hs[0][2] = ek;
   Hs[1][0] = eh; Hs[1][1] = eh; Hs[1][2] = ek;
   Hs[2][0] = ek; Hs[2][1] = ek; Hs[2][2] = ek;
 }
 
-// Dense form (row-major 14x14 Hessian), used by the host checks.
+// Dense form (row-major 14x14 Hessian) used by host checks and the eval hooks.
 MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double* hxx) {
-  int id[3];
   double Hs[3][3];
-  wb_touchdown_compact(x, f, h, hx, id, Hs);
+  if (f == kFront) wb_touchdown_compact<kFront>(x, h, hx, Hs);
+  else wb_touchdown_compact<kBack>(x, h, hx, Hs);
+  const int id[3] = {2, 3 + 2 * f, 4 + 2 * f};
   for (int i = 0; i < 196; ++i) hxx[i] = 0.0;
   for (int a = 0; a < 3; ++a)
     for (int b = 0; b < 3; ++b) hxx[id[a] * 14 + id[b]] = Hs[a][b];
@@ -323,43 +365,45 @@ MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double*
 
 // Foot Jacobian J (2x7, row-major) and Jdot (2x7) as used by the PD warm start
 // (Jacob_F / Jacob_B; boundingPDControl.cpp:29,35).
-MHPC_HD void wb_foot_jacobian(const double* x, int f, double* J, double* Jd) {
+template <int F>
+MHPC_HD void wb_foot_jacobian_f(const double* x, double* J, double* Jd) {
   WbGeo<double> g;
   wb_geometry(x, g);
   double Jm[2][7], jd[2];
-  wb_foot_jac_full(x, g, f, Jm, jd);
+  wb_foot_jac_full<double, F>(x, g, Jm, jd);
+#pragma unroll
   for (int r = 0; r < 2; ++r)
+#pragma unroll
     for (int i = 0; i < 7; ++i) J[r * 7 + i] = Jm[r][i];
-  // Jdot = d/dt J: columns th, hip, knee carry the rates of the link directions.
-  const double sg = f == kFront ? 1.0 : -1.0;
-  const LegGeo<double>& L = g.leg[f];
+  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  const LegGeo<double>& L = g.leg[F];
   const double thd = x[9];
+#pragma unroll
   for (int i = 0; i < 14; ++i) Jd[i] = 0.0;
   // d/dt of -l*cos a = l sin a * adot ; d/dt of l*sin a = l cos a * adot
   const double kx = kShankLen * L.s2 * L.w2, kz = kShankLen * L.c2 * L.w2;
   const double hx = kThighLen * L.s1 * L.w1 + kx, hz = kThighLen * L.c1 * L.w1 + kz;
-  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+  constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   Jd[0 * 7 + ik] = kx;  Jd[1 * 7 + ik] = kz;
   Jd[0 * 7 + ih] = hx;  Jd[1 * 7 + ih] = hz;
   Jd[0 * 7 + 2] = -sg * kHipX * g.cth * thd + hx;
   Jd[1 * 7 + 2] = sg * kHipX * g.sth * thd + hz;
 }
 
-// Hip-to-foot vector of leg f (PlanarQuadruped::get_leg_ext_vec, PlanarQuadruped.cpp:195-205).
-MHPC_HD void wb_leg_ext(const double* q, int f, double* v) {
-  const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+MHPC_HD void wb_foot_jacobian(const double* x, int f, double* J, double* Jd) {
+  if (f == kFront) wb_foot_jacobian_f<kFront>(x, J, Jd);
+  else wb_foot_jacobian_f<kBack>(x, J, Jd);
+}
+
+// Hip-to-foot vector of leg F (PlanarQuadruped::get_leg_ext_vec, PlanarQuadruped.cpp:195-205).
+template <int F>
+MHPC_HD void wb_leg_ext(const double* q, double* v) {
+  constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   double s1, c1, s2, c2;
   sin_cos(q[2] + q[ih], &s1, &c1);
   sin_cos(q[2] + q[ih] + q[ik], &s2, &c2);
   v[0] = -kThighLen * s1 - kShankLen * s2;
   v[1] = -kThighLen * c1 - kShankLen * c2;
-}
-
-// Hip x position of leg f for the SRB foothold planner (FootholdPlan.h:26-50 via
-// PlanarQuadruped::get_contact_position with the hip link frame).
-MHPC_HD double wb_hip_x(const double* pos3, int f) {
-  const double sg = f == kFront ? 1.0 : -1.0;
-  return pos3[0] + sg * kHipX * cos(pos3[2]);
 }
 
 // ---- single rigid body (PlanarFloatingBase + FBDynamics) ---------------------------

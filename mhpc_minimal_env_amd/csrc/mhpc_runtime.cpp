@@ -224,7 +224,10 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
-  if (e == hipSuccess) e = hipMemset(d.x0, 0, B * 14 * sizeof(double));
+  // zero x0 on the handle's own (non-blocking) stream: a null-stream memset would not be
+  // ordered before mhpc_set_x0's copy on this stream
+  if (e == hipSuccess) e = hipMemsetAsync(d.x0, 0, B * 14 * sizeof(double), h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   byte_model(h);
   if (e != hipSuccess) {
     if (h->dcnt) (void)hipFree(h->dcnt);
@@ -281,6 +284,18 @@ static int collect_profile(mhpc_handle* h) {
   h->evkind.clear();
   return MHPC_OK;
 }
+
+// Device -> host copy ordered on the handle's stream.
+static int d2h(mhpc_handle* h, void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return MHPC_OK;
+}
+#define D2H(dst, src, bytes)                \
+  do {                                      \
+    int rc_ = d2h(h, (dst), (src), (bytes)); \
+    if (rc_) return rc_;                    \
+  } while (0)
 
 // initialization(): memory_reset + build_problem (refs) + warmstart, all on the device.
 static int initialize_async(mhpc_handle* h) {
@@ -361,7 +376,7 @@ extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
                       c[C_PX_READS] * kBwsPx;
   if (status) {
     std::vector<ProbState> st(h->sp.B);
-    HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
+    D2H(st.data(), h->d.st, st.size() * sizeof(ProbState));
     for (int b = 0; b < h->sp.B; ++b) status[b] = st[b].status;
   }
   return MHPC_OK;
@@ -395,20 +410,20 @@ extern "C" int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, d
   }
   if (K) {
     std::vector<double> buf(B * NK * 56);
-    HIPCHK(hipMemcpy(buf.data(), h->d.K, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    D2H(buf.data(), h->d.K, buf.size() * sizeof(double));
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
         memcpy(&K[(b * N + k) * 4 * n], &buf[(b * NK + ko + k) * 56], 4 * n * sizeof(double));
   }
   if (du) {
     std::vector<double> buf(B * NK * 4);
-    HIPCHK(hipMemcpy(buf.data(), h->d.du, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    D2H(buf.data(), h->d.du, buf.size() * sizeof(double));
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k) memcpy(&du[(b * N + k) * 4], &buf[(b * NK + ko + k) * 4], 4 * sizeof(double));
   }
   if (Vx) {
     std::vector<double> buf(B * NK * 14);
-    HIPCHK(hipMemcpy(buf.data(), h->d.G, buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+    D2H(buf.data(), h->d.G, buf.size() * sizeof(double));
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
         memcpy(&Vx[(b * N + k) * n], &buf[(b * NK + ko + k) * 14], n * sizeof(double));
@@ -423,7 +438,7 @@ extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, doubl
   HIPCHK(hipSetDevice(h->device));
   const SolveParams& sp = h->sp;
   std::vector<ProbState> st(sp.B);
-  HIPCHK(hipMemcpy(st.data(), h->d.st, st.size() * sizeof(ProbState), hipMemcpyDeviceToHost));
+  D2H(st.data(), h->d.st, st.size() * sizeof(ProbState));
   for (int b = 0; b < sp.B; ++b) {
     if (J) J[b] = st[b].J;
     if (dV_exp) dV_exp[b] = st[b].dV_exp;

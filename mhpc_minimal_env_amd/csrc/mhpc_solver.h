@@ -9,9 +9,11 @@
 //   refpos [B][NK]             forward position reference (ReferenceGen.h:94-109); the
 //          rest of the reference is constant per mode and computed in registers.
 //   K      [B][NK][56], du [B][NK][4], G [B][NK][14]   CostToGoStruct outputs per knot.
-//   par    [B][NK][PS]         dynamics Jacobians of the nominal trajectory, PS = 162 =
-//          18 tangent directions x (7 qddot rows + 2 contact-force rows) per WB knot
-//          (SRB knots are differentiated in registers by the backward kernel).
+//   par    [B][NK][PS]         dynamics Jacobians of the nominal trajectory: 18 tangent
+//          directions x (7 qddot rows + 2 contact-force rows) per WB knot, followed by the
+//          knot's control/force cost derivatives incl. the ReB barrier (computed once per
+//          partials pass, so the backward kernel evaluates no transcendental); SRB knots
+//          are differentiated in registers by the backward kernel.
 //   px     [B][P][196]         impact Jacobian Px (column-major) at the end of WB phases.
 //   state  [B]                 ProbState (control flow + AL/ReB parameters).
 #pragma once
@@ -22,7 +24,9 @@
 namespace mhpc {
 
 constexpr int KS = 24;        // doubles per knot record in traj
-constexpr int PS = 162;       // doubles per knot in par
+constexpr int PS_JAC = 162;   // 18 tangent directions x (7 qddot + 2 contact-force rows)
+constexpr int PS = 176;       // doubles per knot in par: Jacobians + 14 cost derivatives
+                              // (lu 4, luu 4, ly 2, lyy 4 of the stance block)
 constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
 constexpr int TRACE = MHPC_TRACE_LEN;
