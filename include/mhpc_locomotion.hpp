@@ -1,0 +1,192 @@
+// mhpc_locomotion.hpp -- C++ host surface of the reference controller over the C-ABI.
+//
+// Same names, fields and defaults as the reference's API so that the reference's driver
+// (test_main.cpp:12-35) compiles against it unchanged except for the include:
+//   HSDDP_OPTION<T>        MHPC_CompoundTypes.h:196-212
+//   USRCMD                 MHPC_CompoundTypes.h:237-240
+//   MHPCUserParameters     MHPC_CompoundTypes.h:242-251  (alias MHPC_UserParameter)
+//   GaitType2D, Gait       Gait.h:6-77
+//   MHPCLocomotion<T>      MHPCLocomotion.h:13-83 (initialization, solve_mhpc, print_debugInfo)
+// The heavy lifting happens in libmhpc_amd.so (HIP, gfx950).  Extensions: a batch of
+// independent problems per object, and set_initial_conditions() for per-problem x0.
+// Header-only; link with -lmhpc_amd.  Errors throw std::runtime_error on this side of
+// the ABI (none cross it).
+#pragma once
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mhpc_capi.h"
+
+template <typename T>
+struct HSDDP_OPTION {
+  T alpha = 0.1;
+  T gamma = 0.01;
+  T update_penalty = 8;
+  T update_relax = 0.1;
+  T update_regularization = 2;
+  T update_ReB = 7;
+  T max_DDP_iter = 3;
+  T max_AL_iter = 2;
+  T DDP_thresh = 1e-03;
+  T AL_thresh = 1e-03;
+  bool AL_active = 1;
+  bool ReB_active = 1;
+  bool smooth_active = 0;
+};
+
+struct USRCMD {
+  float vel, height, roll, pitch, yaw;
+};
+
+struct MHPCUserParameters {
+  int n_wbphase = 4;
+  int n_fbphase = 4;
+  float dt_wb = .001;
+  float dt_fb = .001;
+  int cmode = 1;
+  float groundH = -0.404;  // unused, as in the reference (ground hard-coded at -0.404)
+  USRCMD* usrcmd = nullptr;
+};
+using MHPC_UserParameter = MHPCUserParameters;
+
+enum class GaitType2D { STAND, BOUND, PRONK };
+
+class Gait {
+ public:
+  Gait() : mode_{1, 2, 3, 4}, timing_{0.08f, 0.1f, 0.08f, 0.1f} {}
+  explicit Gait(GaitType2D g) : mode_{1, 2, 3, 4} {
+    if (g == GaitType2D::BOUND) timing_ = {0.08f, 0.1f, 0.08f, 0.1f};
+    else timing_ = {0.08f, 0.08f, 0.08f, 0.08f};  // default branch of the reference switch
+  }
+  int get_next_mode(int current_mode) const {
+    for (size_t i = 0; i < mode_.size(); ++i)
+      if (mode_[i] == current_mode) return mode_[(i + 1) % mode_.size()];
+    throw std::runtime_error("mode not in gait");
+  }
+  std::vector<int> get_mode_seq(int current_mode, int num_phases) const {
+    std::vector<int> s(num_phases);
+    s[0] = current_mode;
+    for (int p = 0; p + 1 < num_phases; ++p) s[p + 1] = get_next_mode(s[p]);
+    return s;
+  }
+  std::vector<float> get_timings(const std::vector<int>& seq) const {
+    std::vector<float> t(seq.size());
+    for (size_t i = 0; i < seq.size(); ++i) t[i] = timing_[seq[i] - 1];
+    return t;
+  }
+
+ private:
+  std::vector<int> mode_;
+  std::vector<float> timing_;
+};
+
+template <typename TH>
+class MHPCLocomotion {
+ public:
+  // MHPCLocomotion(MHPCUserParameters*, Gait*, HSDDP_OPTION<TH>)  (MHPCLocomotion.cpp:8-43)
+  MHPCLocomotion(MHPCUserParameters* params, Gait* gait, HSDDP_OPTION<TH> option, int batch = 1,
+                 int device = 0)
+      : batch_(batch) {
+    static_assert(sizeof(TH) == 8, "only the double instantiation exists (as in the reference)");
+    const int np = params->n_wbphase + params->n_fbphase;
+    desc_ = mhpc_problem_desc{};
+    desc_.n_wb = params->n_wbphase;
+    desc_.n_fb = params->n_fbphase;
+    desc_.dt_wb = (double)params->dt_wb;
+    desc_.dt_fb = (double)params->dt_fb;
+    desc_.vel_cmd = params->usrcmd ? params->usrcmd->vel : 0.f;
+    desc_.height_cmd = params->usrcmd ? params->usrcmd->height : 0.f;
+    desc_.precision = 64;
+    const std::vector<int> seq = gait->get_mode_seq(params->cmode, np);
+    const std::vector<float> tim = gait->get_timings(seq);
+    for (int p = 0; p < np && p < MHPC_MAX_PHASES; ++p) {  // build_problem (:63-104)
+      desc_.mode_seq[p] = seq[p];
+      // float timing / (double)(float dt), as the reference's DVec<float> / double member
+      desc_.N[p] = (int)std::round((double)tim[p] / (p < desc_.n_wb ? desc_.dt_wb : desc_.dt_fb));
+    }
+    opt_ = mhpc_hsddp_option{option.alpha, option.gamma, option.update_penalty,
+                             option.update_relax, option.update_regularization,
+                             option.update_ReB, option.max_DDP_iter, option.max_AL_iter,
+                             option.DDP_thresh, option.AL_thresh, option.AL_active,
+                             option.ReB_active, option.smooth_active, 0};
+    check(mhpc_create(&desc_, &opt_, batch_, device, &h_), "mhpc_create");
+    // default initial condition (MHPCLocomotion.cpp:37-39), projected if phase 0 is SRB
+    const double x0[14] = {0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098,
+                           0.9011, 0.2756,  0.7333,  0.0446, 0.0009,  1.3219, 2.7346};
+    const int n0 = desc_.n_wb > 0 ? 14 : 6;
+    const int proj[6] = {0, 1, 2, 7, 8, 9};
+    x0_.resize((size_t)batch_ * n0);
+    for (int b = 0; b < batch_; ++b)
+      for (int i = 0; i < n0; ++i) x0_[(size_t)b * n0 + i] = n0 == 14 ? x0[i] : x0[proj[i]];
+  }
+  ~MHPCLocomotion() { mhpc_destroy(h_); }
+  MHPCLocomotion(const MHPCLocomotion&) = delete;
+  MHPCLocomotion& operator=(const MHPCLocomotion&) = delete;
+
+  // extension: per-problem initial states [batch][xsize of phase 0]
+  void set_initial_conditions(const std::vector<double>& x0) { x0_ = x0; }
+
+  void initialization() {  // (:47-53)
+    check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
+    check(mhpc_initialize(h_), "mhpc_initialize");
+  }
+
+  void solve_mhpc() {  // (:167-195)
+    status_.assign(batch_, 0);
+    check(mhpc_solve(h_, status_.data()), "mhpc_solve");
+    std::vector<double> J(batch_), dV(batch_), viol(batch_);
+    check(mhpc_get_scalars(h_, J.data(), dV.data(), viol.data(), nullptr, nullptr, nullptr),
+          "mhpc_get_scalars");
+    _actual_cost = J[0];
+    _exp_cost_change = dV[0];
+    _tconstr_violation = viol[0];
+  }
+
+  // state.txt / control.txt / gradient.txt of problem 0 (MHPCLocomotion.cpp:293-380)
+  void print_debugInfo(int problem = 0) {
+    std::ofstream fx("state.txt"), fu("control.txt"), fg("gradient.txt");
+    for (int p = 0; p < desc_.n_wb + desc_.n_fb; ++p) {
+      int n = 0, N = 0;
+      check(mhpc_phase_dims(&desc_, p, &n, &N), "mhpc_phase_dims");
+      std::vector<double> x((size_t)batch_ * N * n), u((size_t)batch_ * N * 4),
+          g((size_t)batch_ * N * n);
+      check(mhpc_get_phase(h_, p, x.data(), u.data(), nullptr, nullptr, nullptr, g.data()),
+            "mhpc_get_phase");
+      for (int k = 0; k < N; ++k) {
+        write_row(fx, &x[((size_t)problem * N + k) * n], n);
+        write_row(fu, &u[((size_t)problem * N + k) * 4], 4);
+        write_row(fg, &g[((size_t)problem * N + k) * n], n);
+      }
+    }
+  }
+
+  const std::vector<int32_t>& status() const { return status_; }
+  mhpc_handle* handle() { return h_; }
+
+  TH _actual_cost = 0, _exp_cost_change = 0, _tconstr_violation = 0;
+
+ private:
+  static void check(int rc, const char* what) {
+    if (rc != MHPC_OK)
+      throw std::runtime_error(std::string(what) + ": " + mhpc_last_error());
+  }
+  static void write_row(std::ofstream& f, const double* v, int n) {
+    char buf[32];
+    for (int i = 0; i < n; ++i) {
+      std::snprintf(buf, sizeof buf, "%g", v[i]);  // Eigen's default 6 significant digits
+      f << (i ? " " : "") << buf;
+    }
+    f << "\n";
+  }
+
+  int batch_;
+  mhpc_problem_desc desc_;
+  mhpc_hsddp_option opt_;
+  mhpc_handle* h_ = nullptr;
+  std::vector<double> x0_;
+  std::vector<int32_t> status_;
+};

@@ -6,6 +6,7 @@ C3  2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(GaitType2D::PRONK) = default bran
     uniform 0.08 s, dt = (float)0.001 -> N = 80 each; "trot" in BASELINE.json
 C4  = C3, sharded over GPUs
 C5  Gait() BOUND, 4 WB + 6 SRB (fp32 in BASELINE.json; fp64 here until the fp32 path lands)
+demo  test_main.cpp: default MHPCUserParameters (4 WB + 4 SRB), Gait() BOUND, default x0
 """
 from __future__ import annotations
 
@@ -33,6 +34,11 @@ def c3_desc():
 def c5_desc():
     params = L.MHPCUserParameters(n_wbphase=4, n_fbphase=6, usrcmd=L.USRCMD(vel=1.5))
     return L.desc_from_params(params, L.Gait())
+
+
+def demo_desc():
+    """test_main.cpp's problem: default MHPCUserParameters (4 WB + 4 SRB), Gait() BOUND."""
+    return L.desc_from_params(L.MHPCUserParameters(usrcmd=L.USRCMD(vel=1.5)), L.Gait())
 
 
 def x0_for(desc, batch: int, offset: int = 0):
