@@ -1,0 +1,56 @@
+"""Per-kernel HBM traffic from rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE, KB per
+dispatch) -> profiles/pmc_traffic.json.  gfx950 correction (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE counts 64 B per 128-B request of a wide coalesced read, i.e. half the bytes; it
+is doubled here (an upper estimate for this code's 8-B-per-lane reads, whose calibration
+the guide leaves open -- the raw value is kept beside it).
+usage: python tools/pmc_summary.py <prof_dir> <out.json> [note]"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+SHORT = {"k_bws": "k_bws", "k_partials": "k_partials", "k_init": "k_init", "k_al_end": "k_al_end",
+         "k_rollout": "k_rollout", "k_reduce_counters": "k_reduce_counters"}
+
+
+def load(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            m = re.search(r"mhpc::(\w+)", name)
+            key = m.group(1) if m else name
+            if key == "k_rollout":  # full sweep (1 lane / problem) vs line search grids
+                key = f"k_rollout[grid={r['Grid_Size']}]"
+            acc[key].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    note = sys.argv[3] if len(sys.argv) > 3 else ""
+    fetch = load(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = load(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, [0.0])
+        w = write.get(k, [0.0])
+        fb = sum(f) / len(f) * 1024
+        wb = sum(w) / len(w) * 1024
+        res[k] = {"dispatches": len(f), "fetch_bytes_raw": fb, "write_bytes": wb,
+                  "hbm_bytes_per_launch": 2 * fb + wb}
+    doc = {"source": d, "note": note, "correction": "hbm = 2 * FETCH_SIZE*1024 + WRITE_SIZE*1024",
+           "kernels": res}
+    with open(out, "w") as fo:
+        json.dump(doc, fo, indent=1)
+    for k, v in res.items():
+        print(f"{k:32s} n={v['dispatches']:3d} fetch={v['fetch_bytes_raw']/1e6:10.2f} MB "
+              f"write={v['write_bytes']/1e6:10.2f} MB  hbm/launch={v['hbm_bytes_per_launch']/1e6:10.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
