@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmhpc_amd.so")
+# MHPC_AMD_LIB: alternate build of the same library (tuning experiments)
+LIB_PATH = os.environ.get("MHPC_AMD_LIB") or os.path.join(HERE, "libmhpc_amd.so")
 
 MHPC_MAX_PHASES = 16
 MHPC_MAX_KNOTS = 1024

@@ -169,55 +169,125 @@ __device__ __forceinline__ int coef_b(int col) {
 
 // One Riccati knot.  On entry sh.{W,G2,l,lxx,luu,lyy2,ly2} hold the knot's derivatives and
 // sh.{H,G} the value function of knot k+1; on exit sh.{H,G} hold that of knot k.
+#ifndef MHPC_BWS_CH2
+#define MHPC_BWS_CH2 3
+#endif
+#ifndef MHPC_BWS_CH3
+#define MHPC_BWS_CH3 3
+#endif
+#ifndef MHPC_BWS_CH5
+#define MHPC_BWS_CH5 4
+#endif
+constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
+
 template <int NQ, bool HAS_Y>
 __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9,
                              double* Kout, double* duout, double* Gout) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
-  // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly
-  #pragma unroll 1
-  for (int e = lane; e < NR * NX + NR; e += 64) {
-    if (e < NR * NX) {
-      const int row = e / NX, j = e - row * NX;
-      const double a = coef_a<NQ>(row, dt);
-      double s = 0.0;
-      if (a != 0.0) s = a * sh.H[coef_b<NQ>(row) * NX + j];
+  // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly.
+  // Lane = (column j of H, row group g): the column H[NQ.., j] stays in registers and the
+  // lane runs up to RPL independent row chains (ILP); the last QL lanes build Qv.
+  {
+    constexpr int QL = NX == 14 ? 8 : 10;     // lanes for Qv
+    constexpr int G = (64 - QL) / NX;          // row groups
+    constexpr int RPL = (NR + G - 1) / G;      // rows per lane
+    if (lane < G * NX) {
+      const int j = lane % NX, g = lane / NX;
+      double hc[NQ];
 #pragma unroll
-      for (int r = 0; r < NQ; ++r) s += sh.W[r * NR + row] * sh.H[(NQ + r) * NX + j];
-      sh.Jt[e] = s;
+      for (int r = 0; r < NQ; ++r) hc[r] = sh.H[(NQ + r) * NX + j];
+      constexpr int C = RPL < CH2 ? RPL : CH2;  // chains in flight
+#pragma unroll 1
+      for (int t0 = 0; t0 < RPL; t0 += C) {
+        double acc[C];
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int row = g + G * (t0 + u);
+          double sacc = 0.0;
+          if (row < NR) {
+            const double a = coef_a<NQ>(row, dt);
+            if (a != 0.0) sacc = a * sh.H[coef_b<NQ>(row) * NX + j];
+#pragma unroll
+            for (int r = 0; r < NQ; ++r) sacc += sh.W[r * NR + row] * hc[r];
+          }
+          acc[u] = sacc;
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int row = g + G * (t0 + u);
+          if (row < NR) sh.Jt[row * NX + j] = acc[u];
+        }
+      }
     } else {
-      const int row = e - NR * NX;
-      const double a = coef_a<NQ>(row, dt);
-      double s = 0.0, t = 0.0;
-      if (a != 0.0) s = a * sh.G[coef_b<NQ>(row)];
+      const int q = lane - G * NX;
+      double gc[NQ];
 #pragma unroll
-      for (int r = 0; r < NQ; ++r) s += sh.W[r * NR + row] * sh.G[NQ + r];
-      if (HAS_Y) t = sh.G2[row] * sh.ly2[0] + sh.G2[NR + row] * sh.ly2[1];
-      sh.Qv[row] = (sh.l[row] + s) + t;
+      for (int r = 0; r < NQ; ++r) gc[r] = sh.G[NQ + r];
+#pragma unroll
+      for (int t = 0; t < (NR + QL - 1) / QL; ++t) {
+        const int row = q + QL * t;
+        if (row < NR) {
+          const double a = coef_a<NQ>(row, dt);
+          double sacc = 0.0, tt = 0.0;
+          if (a != 0.0) sacc = a * sh.G[coef_b<NQ>(row)];
+#pragma unroll
+          for (int r = 0; r < NQ; ++r) sacc += sh.W[r * NR + row] * gc[r];
+          if (HAS_Y) tt = sh.G2[row] * sh.ly2[0] + sh.G2[NR + row] * sh.ly2[1];
+          sh.Qv[row] = (sh.l[row] + sacc) + tt;
+        }
+      }
     }
   }
   __syncthreads();
   // R3: Qxx = (lxx + C'lyy C) + A'HA ; Qux = (0 + D'lyy C) + B'HA ; Quu = (luu + D'lyy D) + B'HB
-  #pragma unroll 1
-  for (int e = lane; e < NX * NX + 4 * NR; e += 64) {
-    int row, col;
-    if (e < NX * NX) { row = e / NX; col = e - row * NX; }
-    else { const int q = e - NX * NX; row = NX + q / NR; col = q - (q / NR) * NR; }
-    const double a = coef_a<NQ>(col, dt);
-    double s = 0.0;
-    if (a != 0.0) s = a * sh.Jt[row * NX + coef_b<NQ>(col)];
+  // Lane = (row of Jt, column group g): the row Jt[row, NQ..] stays in registers, up to CPL
+  // independent column chains per lane.
+  {
+    constexpr int RG = 64 / NR;                    // column groups
+    constexpr int CPL = (NR + RG - 1) / RG;        // columns per lane
+    if (lane < RG * NR) {
+      const int row = lane % NR, g = lane / NR;
+      const int ncol = row < NX ? NX : NR;
+      double jr[NQ];
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) s += sh.Jt[row * NX + NQ + r] * sh.W[r * NR + col];
-    double base = 0.0;
-    if (row == col) base = row < NX ? sh.lxx[row] : sh.luu[row - NX];
-    double e2 = 0.0;
-    if (HAS_Y) {
-      const double c0 = sh.G2[row] * sh.lyy2[0] + sh.G2[NR + row] * sh.lyy2[2];
-      const double c1 = sh.G2[row] * sh.lyy2[1] + sh.G2[NR + row] * sh.lyy2[3];
-      e2 = c0 * sh.G2[col] + c1 * sh.G2[NR + col];
+      for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
+      double gr0 = 0.0, gr1 = 0.0, c0 = 0.0, c1 = 0.0;
+      if (HAS_Y) {
+        gr0 = sh.G2[row];
+        gr1 = sh.G2[NR + row];
+        c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
+        c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
+      }
+      constexpr int C = CPL < CH3 ? CPL : CH3;
+#pragma unroll 1
+      for (int t0 = 0; t0 < CPL; t0 += C) {
+        double acc[C];
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int col = g + RG * (t0 + u);
+          double v = 0.0;
+          if (col < ncol) {
+            const double a = coef_a<NQ>(col, dt);
+            double sacc = 0.0;
+            if (a != 0.0) sacc = a * sh.Jt[row * NX + coef_b<NQ>(col)];
+#pragma unroll
+            for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * NR + col];
+            double base = 0.0;
+            if (row == col) base = row < NX ? sh.lxx[row] : sh.luu[row - NX];
+            double e2 = 0.0;
+            if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[NR + col];
+            v = (base + e2) + sacc;
+            if (row == col) v += 1.0 * reg;
+          }
+          acc[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int col = g + RG * (t0 + u);
+          if (col < ncol) sh.Q[row * NR + col] = acc[u];
+        }
+      }
     }
-    double v = (base + e2) + s;
-    if (row == col && (row < NX || col >= NX)) v += 1.0 * reg;
-    sh.Q[row * NR + col] = v;
   }
   __syncthreads();
   // R4: PSD test of Quu - 1e-9 I (every lane, registers, static indices), then the
@@ -290,23 +360,47 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     }
   }
   __syncthreads();
-  // R5: H = sym(Qxx) - tq Qux ; G = Qx - tq Qu
-  #pragma unroll 1
-  for (int e = lane; e < NX * NX + NX; e += 64) {
-    if (e < NX * NX) {
-      const int i = e / NX, j = e - i * NX;
-      double s = 0;
+  // R5: H = sym(Qxx) - tq Qux ; G = Qx - tq Qu.  Lane = (column j, row group): the column
+  // Qux[., j] stays in registers, up to 4 independent row chains per lane.
+  {
+    constexpr int G5 = 56 / NX;               // 4 for NX = 14, 9 for NX = 6
+    constexpr int R5 = (NX + G5 - 1) / G5;
+    if (lane < G5 * NX) {
+      const int j = lane % NX, g = lane / NX;
+      double qc[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) s += sh.tq[i * 4 + c] * sh.Q[(NX + c) * NR + j];
-      sh.H[e] = (sh.Q[i * NR + j] + sh.Q[j * NR + i]) / 2 - s;
+      for (int c = 0; c < 4; ++c) qc[c] = sh.Q[(NX + c) * NR + j];
+      constexpr int C = R5 < CH5 ? R5 : CH5;
+#pragma unroll 1
+      for (int t0 = 0; t0 < R5; t0 += C) {
+        double acc[C];
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int i = g + G5 * (t0 + u);
+          double v = 0.0;
+          if (i < NX) {
+            double sacc = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sacc += sh.tq[i * 4 + c] * qc[c];
+            v = (sh.Q[i * NR + j] + sh.Q[j * NR + i]) / 2 - sacc;
+          }
+          acc[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+          const int i = g + G5 * (t0 + u);
+          if (i < NX) sh.H[i * NX + j] = acc[u];
+        }
+      }
     } else {
-      const int i = e - NX * NX;
-      double s = 0;
+      for (int i = lane - G5 * NX; i < NX; i += 64 - G5 * NX) {
+        double sacc = 0;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) s += sh.tq[i * 4 + c] * sh.Qv[NX + c];
-      const double g = sh.Qv[i] - s;
-      sh.G[i] = g;
-      Gout[i] = g;
+        for (int c = 0; c < 4; ++c) sacc += sh.tq[i * 4 + c] * sh.Qv[NX + c];
+        const double gi = sh.Qv[i] - sacc;
+        sh.G[i] = gi;
+        Gout[i] = gi;
+      }
     }
   }
   __syncthreads();

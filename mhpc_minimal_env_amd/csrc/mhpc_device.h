@@ -50,17 +50,20 @@ static __device__ __forceinline__ double* traj_ptr(const SolveParams& sp, const 
 static __device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (mode == 2 || mode == 4); }
 
 // ---- reduced barrier (SinglePhase.cpp:298-317), k = 2 ---------------------------------
+// The reference's pow() calls with integer exponents are evaluated exactly as products:
+// pow(t, 2) = t*t (the correctly rounded square), pow(t, 1) = t, pow(t, 0) = 1 (also for
+// NaN, as pow defines), pow(g, -2) = 1/(g*g) (within 1 ulp of the correctly rounded value).
 static __device__ __forceinline__ void reduced_barrier(double g, double delta, double* B, double* Bz,
                                                 double* Bzz) {
   if (g > delta) {
     *B = -log(g);
     *Bz = -1.0 / g;
-    *Bzz = pow(g, -2.0);
+    *Bzz = 1.0 / (g * g);
   } else {
     const double t = (g - 2 * delta) / ((2 - 1) * delta);
-    *B = (double)(2 - 1) / 2 * (pow(t, 2.0) - 1) - log(delta);
-    *Bz = pow(t, 1.0) / delta;
-    *Bzz = pow(t, 0.0);
+    *B = (double)(2 - 1) / 2 * (t * t - 1) - log(delta);
+    *Bz = t / delta;
+    *Bzz = 1.0;
   }
 }
 

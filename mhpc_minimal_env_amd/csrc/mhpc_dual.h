@@ -55,11 +55,16 @@ MHPC_HD double val(double a) { return a; }
 MHPC_HD double val(Dual a) { return a.v; }
 
 MHPC_HD void sin_cos(double a, double* s, double* c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  sincos(a, s, c);  // one shared argument reduction on the device
+#else
   *s = sin(a);
   *c = cos(a);
+#endif
 }
 MHPC_HD void sin_cos(Dual a, Dual* s, Dual* c) {
-  const double sv = sin(a.v), cv = cos(a.v);
+  double sv, cv;
+  sin_cos(a.v, &sv, &cv);
   *s = Dual(sv, cv * a.d);
   *c = Dual(cv, -sv * a.d);
 }

@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
           h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
           if (sp.AL_active) {
             const double s = st->sigma[p], lam = st->lambda[p];
-            Phi += 50 * (pow(s * h / 2, 2.0) + lam * h);
+            const double sh2 = s * h / 2;
+            Phi += 50 * (sh2 * sh2 + lam * h);
           }
         }
         V += Phi;

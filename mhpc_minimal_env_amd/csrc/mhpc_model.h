@@ -15,8 +15,8 @@
 // front/back hips sit at (x +- 0.19 cos th, z -+ 0.19 sin th).  M(q) and the bias
 // h(q, qdot) are assembled body by body from CoM Jacobians (M = sum m Jc'Jc + Ic w w',
 // h = sum m Jc'(Jcdot qdot + g)), which is exact for a planar tree.  Stance and impact
-// solve the contact KKT system through the Schur complement J M^-1 J' of a Cholesky
-// factor of M (the reference's generated code uses an unpivoted QR instead; both agree
+// solve the contact KKT system through the Schur complement J M^-1 J' of a block-arrowhead
+// factorisation of M (the reference's generated code uses an unpivoted QR instead; both agree
 // to ~1e-12, see tests/test_model_host.py).
 //
 // Everything is templated on the scalar so the same source runs in double (rollouts)
@@ -165,41 +165,83 @@ MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
   add_leg<S, kBack>(x, g, M, h);
 }
 
-// In-place Cholesky M = L L' on the packed lower triangle.
+// Block-arrowhead factorisation of the mass matrix.  Ordered (base x,z,th | front leg |
+// back leg), M has no front/back-leg coupling, so it is solved by eliminating the two 2x2
+// leg blocks first and factoring the 3x3 base Schur complement S (no fill-in, three
+// reciprocals, no square roots) -- the tree structure an articulated-body solver exploits.
 template <class S>
-MHPC_HD void chol7(S A[28]) {
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    S d = A[tri(j, j)];
-#pragma unroll
-    for (int k = 0; k < j; ++k) d -= A[tri(j, k)] * A[tri(j, k)];
-    const S l = sqrt_(d);
-    A[tri(j, j)] = l;
-#pragma unroll
-    for (int i = j + 1; i < 7; ++i) {
-      S s = A[tri(i, j)];
-#pragma unroll
-      for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
-      A[tri(i, j)] = s / l;
-    }
-  }
-}
+struct ArrowFactor {
+  S Li[2][3];   // inverse of each 2x2 leg block (a, b, c of [[a b][b c]]^-1)
+  S Z[2][2][3]; // Z_l = Ml^-1 * M_lb  (2 x 3)
+  S Si[6];      // inverse of the base Schur complement, packed symmetric (00,10,11,20,21,22)
+};
 
 template <class S>
-MHPC_HD void chol7_solve(const S L[28], S b[7]) {
+MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
+  // base Schur complement S = Mbb - sum_l Mlb' Ml^-1 Mlb (symmetric, lower packed)
+  S s00 = M[tri(0, 0)], s10 = M[tri(1, 0)], s11 = M[tri(1, 1)];
+  S s20 = M[tri(2, 0)], s21 = M[tri(2, 1)], s22 = M[tri(2, 2)];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    S s = b[i];
+  for (int l = 0; l < 2; ++l) {
+    const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
+    const S a = M[tri(i0, i0)], b = M[tri(i1, i0)], c = M[tri(i1, i1)];
+    const S rdet = S(1.0) / (a * c - b * b);
+    F.Li[l][0] = c * rdet;
+    F.Li[l][1] = -b * rdet;
+    F.Li[l][2] = a * rdet;
 #pragma unroll
-    for (int k = 0; k < i; ++k) s -= L[tri(i, k)] * b[k];
-    b[i] = s / L[tri(i, i)];
+    for (int j = 0; j < 3; ++j) {
+      const S m0 = M[tri(i0, j)], m1 = M[tri(i1, j)];
+      F.Z[l][0][j] = F.Li[l][0] * m0 + F.Li[l][1] * m1;
+      F.Z[l][1][j] = F.Li[l][1] * m0 + F.Li[l][2] * m1;
+    }
+    // S -= Mlb' Z
+    const S* z0 = F.Z[l][0];
+    const S* z1 = F.Z[l][1];
+    s00 -= M[tri(i0, 0)] * z0[0] + M[tri(i1, 0)] * z1[0];
+    s10 -= M[tri(i0, 1)] * z0[0] + M[tri(i1, 1)] * z1[0];
+    s11 -= M[tri(i0, 1)] * z0[1] + M[tri(i1, 1)] * z1[1];
+    s20 -= M[tri(i0, 2)] * z0[0] + M[tri(i1, 2)] * z1[0];
+    s21 -= M[tri(i0, 2)] * z0[1] + M[tri(i1, 2)] * z1[1];
+    s22 -= M[tri(i0, 2)] * z0[2] + M[tri(i1, 2)] * z1[2];
   }
+  // 3x3 symmetric inverse by cofactors
+  const S c00 = s11 * s22 - s21 * s21;
+  const S c10 = s21 * s20 - s10 * s22;
+  const S c20 = s10 * s21 - s11 * s20;
+  const S rdet = S(1.0) / (s00 * c00 + s10 * c10 + s20 * c20);
+  F.Si[0] = c00 * rdet;
+  F.Si[1] = c10 * rdet;
+  F.Si[2] = (s00 * s22 - s20 * s20) * rdet;
+  F.Si[3] = c20 * rdet;
+  F.Si[4] = (s20 * s10 - s00 * s21) * rdet;
+  F.Si[5] = (s00 * s11 - s10 * s10) * rdet;
+}
+
+// b <- M^-1 b
+template <class S>
+MHPC_HD void arrow_solve(const S M[28], const ArrowFactor<S>& F, S b[7]) {
+  S w[2][2];
+  S r0 = b[0], r1 = b[1], r2 = b[2];
 #pragma unroll
-  for (int i = 6; i >= 0; --i) {
-    S s = b[i];
+  for (int l = 0; l < 2; ++l) {
+    const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
+    w[l][0] = F.Li[l][0] * b[i0] + F.Li[l][1] * b[i1];
+    w[l][1] = F.Li[l][1] * b[i0] + F.Li[l][2] * b[i1];
+    r0 -= M[tri(i0, 0)] * w[l][0] + M[tri(i1, 0)] * w[l][1];
+    r1 -= M[tri(i0, 1)] * w[l][0] + M[tri(i1, 1)] * w[l][1];
+    r2 -= M[tri(i0, 2)] * w[l][0] + M[tri(i1, 2)] * w[l][1];
+  }
+  const S x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
+  const S x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
+  const S x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
+  b[0] = x0;
+  b[1] = x1;
+  b[2] = x2;
 #pragma unroll
-    for (int k = i + 1; k < 7; ++k) s -= L[tri(k, i)] * b[k];
-    b[i] = s / L[tri(i, i)];
+  for (int l = 0; l < 2; ++l) {
+    b[3 + 2 * l] = w[l][0] - (F.Z[l][0][0] * x0 + F.Z[l][0][1] * x1 + F.Z[l][0][2] * x2);
+    b[4 + 2 * l] = w[l][1] - (F.Z[l][1][0] * x0 + F.Z[l][1][1] * x1 + F.Z[l][1][2] * x2);
   }
 }
 
@@ -221,15 +263,16 @@ MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, S J[2][7], S jd[2])
 
 // Schur-complement solve of the contact KKT system
 //   [M -J'; J 0] [v; lam] = [rhs; -c]  ->  v = M^-1 (rhs + J' lam)
-// given the Cholesky factor L of M; v holds M^-1 rhs on entry.
+// given the factorisation of M; v holds M^-1 rhs on entry.
 template <class S>
-MHPC_HD void kkt_contact(const S L[28], const S J[2][7], const S c[2], S v[7], S lam[2]) {
+MHPC_HD void kkt_contact(const S M[28], const ArrowFactor<S>& F, const S J[2][7], const S c[2],
+                         S v[7], S lam[2]) {
   S Y[2][7];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) Y[r][i] = J[r][i];
-    chol7_solve(L, Y[r]);
+    arrow_solve(M, F, Y[r]);
   }
   S A00 = S(0.0), A01 = S(0.0), A11 = S(0.0), r0 = -c[0], r1 = -c[1];
 #pragma unroll
@@ -240,19 +283,20 @@ MHPC_HD void kkt_contact(const S L[28], const S J[2][7], const S c[2], S v[7], S
     r0 -= J[0][i] * v[i];
     r1 -= J[1][i] * v[i];
   }
-  const S det = A00 * A11 - A01 * A01;
-  lam[0] = (A11 * r0 - A01 * r1) / det;
-  lam[1] = (A00 * r1 - A01 * r0) / det;
+  const S rdet = S(1.0) / (A00 * A11 - A01 * A01);
+  lam[0] = (A11 * r0 - A01 * r1) * rdet;
+  lam[1] = (A00 * r1 - A01 * r0) * rdet;
 #pragma unroll
   for (int i = 0; i < 7; ++i) v[i] += Y[0][i] * lam[0] + Y[1][i] * lam[1];
 }
 
 // Stance dynamics with foot F on the ground (Dyn_FS: F = front, Dyn_BS: F = back).
 template <class S, int F>
-MHPC_HD void wb_stance(const S* x, const WbGeo<S>& g, const S L[28], S v[7], S* y) {
+MHPC_HD void wb_stance(const S* x, const WbGeo<S>& g, const S M[28], const ArrowFactor<S>& AF,
+                       S v[7], S* y) {
   S J[2][7], jd[2], lam[2];
   wb_foot_jac_full<S, F>(x, g, J, jd);
-  kkt_contact(L, J, jd, v, lam);
+  kkt_contact(M, AF, J, jd, v, lam);
   y[2 * F] = lam[0];
   y[2 * F + 1] = lam[1];
 }
@@ -266,16 +310,17 @@ MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
   wb_geometry(x, g);
   S M[28], h[7];
   wb_mass_bias(x, g, M, h);
-  chol7(M);
+  ArrowFactor<S> AF;
+  arrow_factor(M, AF);
   S v[7];
   v[0] = -h[0]; v[1] = -h[1]; v[2] = -h[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
-  chol7_solve(M, v);
+  arrow_solve(M, AF, v);
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = S(0.0);
-  if (mode == 1) wb_stance<S, kBack>(x, g, M, v, y);
-  else if (mode == 3) wb_stance<S, kFront>(x, g, M, v, y);
+  if (mode == 1) wb_stance<S, kBack>(x, g, M, AF, v, y);
+  else if (mode == 3) wb_stance<S, kFront>(x, g, M, AF, v, y);
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     xdot[i] = x[7 + i];
@@ -291,7 +336,8 @@ MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
   wb_geometry(x, g);
   S M[28], h[7];
   wb_mass_bias(x, g, M, h);
-  chol7(M);
+  ArrowFactor<S> AF;
+  arrow_factor(M, AF);
   S J[2][7], jd[2];
   wb_foot_jac_full<S, F>(x, g, J, jd);
   S v[7], c[2];
@@ -299,7 +345,7 @@ MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
   for (int i = 0; i < 7; ++i) v[i] = x[7 + i];  // M^-1 (M qd-) = qd-
   c[0] = S(0.0);
   c[1] = S(0.0);
-  kkt_contact(M, J, c, v, Lam);  // J qd+ = 0
+  kkt_contact(M, AF, J, c, v, Lam);  // J qd+ = 0
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     xp[i] = x[i];

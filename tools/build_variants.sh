@@ -1,0 +1,15 @@
+# Build alternate copies of libmhpc_amd.so with different compile-time tuning flags into
+# mhpc_minimal_env_amd/csrc/_build/var/<name>/ (travels with the gpurun snapshot).
+# usage: bash tools/build_variants.sh name1 "-DFLAG=.." name2 "-DFLAG=.." ...
+set -e
+C=/root/repo/mhpc_minimal_env_amd/csrc
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  d=$C/_build/var/$name; mkdir -p $d
+  make -s -C $C all >/dev/null
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c -o $d/bws.o $C/mhpc_bws.hip &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c -o $d/kern.o $C/mhpc_kernels.hip &
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libmhpc_amd.so $d/bws.o $d/kern.o $C/_build/mhpc_runtime.o
+  echo "$name: $flags" > $d/FLAGS
+done
