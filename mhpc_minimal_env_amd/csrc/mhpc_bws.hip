@@ -23,17 +23,28 @@
 
 namespace mhpc {
 
+// Padded LDS shapes: every lane of a round runs the same straight-line code; rows / columns
+// past the real extents land in padding that no real output reads.
+constexpr int WS = 20;          // row stride of W / G2 (columns of [A B], padded)
+constexpr int JR = 20;          // rows of Jt (padded)
+constexpr int QR = 20;          // rows of Q (padded)
+template <int NX> struct QShape {
+  static constexpr int NR = NX + 4;
+  static constexpr int QS = NX == 14 ? 19 : 13;  // row stride of Q; column QV holds Qv
+  static constexpr int QV = QS - 1;
+};
+
 struct BwsLds {
   double H[196], G[14];  // value function of knot k+1, then of knot k (row stride NX)
-  double W[7 * 18];      // rows NQ..NX-1 of [A B], stride NR = NX + 4
-  double G2[2 * 18];     // stance rows of [C D]
-  double l[18];          // (lx, lu)
-  double lxx[14], luu[4];
+  double W[7 * WS];      // rows NQ..NX-1 of [A B]
+  double G2[2 * WS];     // stance rows of [C D]
+  double l[JR];          // (lx, lu)
+  double ldiag[18];      // diagonal running-cost Hessian (lxx, luu)
   double lyy2[4], ly2[2];
   union {
     struct {
-      double Jt[18 * 14];  // [A B]' H   (NR x NX)
-      double Q[18 * 18];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu (4x4), stride NR
+      double Jt[JR * 14];  // [A B]' H   (NR x NX)
+      double Q[QR * 19];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
     };
     struct {
       double H2[196];      // impact-aware step: lifted H' and (Px' H2)
@@ -42,13 +53,31 @@ struct BwsLds {
     };
   };
   double Qv[18];         // (Qx, Qu)
-  double Qi[16], inv[16];
-  double tq[14 * 4 + 16];  // Qux' Quu_inv (NX x 4) + scratch for the raw inverse
-  double xb[14], ub[4], yb[4];
+  double xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
+  double Kst[56], dust[4], Gst[14];     // results of the last knot, stored one knot later
   double hx[14], Hs[9], G2v[14];
   double dV;
   int fail;
+#ifdef MHPC_BWS_TIMING
+  unsigned long long cyc[12], tlast;
+#endif
 };
+
+// Optional cycle accounting per Riccati round (build with -DMHPC_BWS_TIMING; read with
+// mhpc_dbg_bws_cycles): slot i accumulates the cycles since the previous mark.
+#ifdef MHPC_BWS_TIMING
+#define BWS_TMARK(sh, lane, i)                          \
+  do {                                                  \
+    if ((lane) == 0) {                                  \
+      const unsigned long long t_ = clock64();          \
+      (sh).cyc[i] += t_ - (sh).tlast;                   \
+      (sh).tlast = t_;                                  \
+    }                                                   \
+  } while (0)
+__device__ unsigned long long g_bws_cyc[12];
+#else
+#define BWS_TMARK(sh, lane, i) do { } while (0)
+#endif
 
 // Eigen-style 4x4 inverse by cofactors (same formulas as the oracle).
 __device__ __forceinline__ void inverse4(const double* m, double* inv) {
@@ -157,6 +186,14 @@ __device__ __forceinline__ bool ldlt_is_positive4(double* A) {
   return sign == 1 || sign == 0;
 }
 
+// Value of lane `src` (uniform) of a double held per lane: two readlanes, no LDS.
+__device__ __forceinline__ double lane_bcast(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // Row coefficient of the exact part of [A B] (see file header).
 template <int NQ>
 __device__ __forceinline__ double coef_a(int col, double dt) {
@@ -181,242 +218,222 @@ __device__ __forceinline__ int coef_b(int col) {
 constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
 
 template <int NQ, bool HAS_Y>
-__device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9,
-                             double* Kout, double* duout, double* Gout) {
+__device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
-  // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly.
-  // Lane = (column j of H, row group g): the column H[NQ.., j] stays in registers and the
-  // lane runs up to RPL independent row chains (ILP); the last QL lanes build Qv.
+  constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
+  // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly, G taken as column NX
+  // of [H | G].  Lane = (column j, row group g): the column stays in registers and the lane
+  // runs T2 independent row chains.
   {
-    constexpr int QL = NX == 14 ? 8 : 10;     // lanes for Qv
-    constexpr int G = (64 - QL) / NX;          // row groups
-    constexpr int RPL = (NR + G - 1) / G;      // rows per lane
-    if (lane < G * NX) {
-      const int j = lane % NX, g = lane / NX;
-      double hc[NQ];
+    constexpr int NC = NX + 1, GR = 64 / NC, T2 = (NR + GR - 1) / GR;
+    const int j = lane % NC, g = lane / NC;
+    const bool isg = j == NX;
+    const double* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
+    const int cs = isg ? 1 : NX;
+    double hc[NQ];
 #pragma unroll
-      for (int r = 0; r < NQ; ++r) hc[r] = sh.H[(NQ + r) * NX + j];
-      constexpr int C = RPL < CH2 ? RPL : CH2;  // chains in flight
+    for (int r = 0; r < NQ; ++r) hc[r] = col0[(NQ + r) * cs];
+    constexpr int C = T2 < CH2 ? T2 : CH2;
 #pragma unroll 1
-      for (int t0 = 0; t0 < RPL; t0 += C) {
-        double acc[C];
+    for (int t0 = 0; t0 < T2; t0 += C) {
+      double acc[C];
 #pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int row = g + G * (t0 + u);
-          double sacc = 0.0;
-          if (row < NR) {
-            const double a = coef_a<NQ>(row, dt);
-            if (a != 0.0) sacc = a * sh.H[coef_b<NQ>(row) * NX + j];
+      for (int u = 0; u < C; ++u) {
+        const int row = g + GR * (t0 + u);  // < JR
+        const double a = coef_a<NQ>(row, dt);
+        const double hb = col0[coef_b<NQ>(row) * cs];
+        double sacc = a != 0.0 ? a * hb : 0.0;
 #pragma unroll
-            for (int r = 0; r < NQ; ++r) sacc += sh.W[r * NR + row] * hc[r];
-          }
-          acc[u] = sacc;
+        for (int r = 0; r < NQ; ++r) sacc += sh.W[r * WS + row] * hc[r];
+        if (isg) {
+          double tt = 0.0;
+          if (HAS_Y) tt = sh.G2[row] * sh.ly2[0] + sh.G2[WS + row] * sh.ly2[1];
+          sacc = (sh.l[row] + sacc) + tt;
         }
-#pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int row = g + G * (t0 + u);
-          if (row < NR) sh.Jt[row * NX + j] = acc[u];
-        }
+        acc[u] = sacc;
       }
-    } else {
-      const int q = lane - G * NX;
-      double gc[NQ];
 #pragma unroll
-      for (int r = 0; r < NQ; ++r) gc[r] = sh.G[NQ + r];
-#pragma unroll
-      for (int t = 0; t < (NR + QL - 1) / QL; ++t) {
-        const int row = q + QL * t;
-        if (row < NR) {
-          const double a = coef_a<NQ>(row, dt);
-          double sacc = 0.0, tt = 0.0;
-          if (a != 0.0) sacc = a * sh.G[coef_b<NQ>(row)];
-#pragma unroll
-          for (int r = 0; r < NQ; ++r) sacc += sh.W[r * NR + row] * gc[r];
-          if (HAS_Y) tt = sh.G2[row] * sh.ly2[0] + sh.G2[NR + row] * sh.ly2[1];
-          sh.Qv[row] = (sh.l[row] + sacc) + tt;
-        }
+      for (int u = 0; u < C; ++u) {
+        const int row = g + GR * (t0 + u);
+        if (t0 + u < T2 && g < GR) *(isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * NX + j]) = acc[u];
       }
     }
   }
   __syncthreads();
+  BWS_TMARK(sh, lane, 1);
   // R3: Qxx = (lxx + C'lyy C) + A'HA ; Qux = (0 + D'lyy C) + B'HA ; Quu = (luu + D'lyy D) + B'HB
-  // Lane = (row of Jt, column group g): the row Jt[row, NQ..] stays in registers, up to CPL
-  // independent column chains per lane.
+  // (+ reg on the diagonal).  Lane = (row of Jt, column group g), the row Jt[row, NQ..] in
+  // registers, T3 independent column chains.
   {
-    constexpr int RG = 64 / NR;                    // column groups
-    constexpr int CPL = (NR + RG - 1) / RG;        // columns per lane
-    if (lane < RG * NR) {
-      const int row = lane % NR, g = lane / NR;
-      const int ncol = row < NX ? NX : NR;
-      double jr[NQ];
+    constexpr int RG = 64 / NR, T3 = NX == 14 ? 6 : 2;  // columns g + RG t < QV
+    const int row = lane % NR, g = lane / NR;
+    double jr[NQ];
 #pragma unroll
-      for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
-      double gr0 = 0.0, gr1 = 0.0, c0 = 0.0, c1 = 0.0;
-      if (HAS_Y) {
-        gr0 = sh.G2[row];
-        gr1 = sh.G2[NR + row];
-        c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
-        c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
-      }
-      constexpr int C = CPL < CH3 ? CPL : CH3;
+    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
+    double c0 = 0.0, c1 = 0.0;
+    if (HAS_Y) {
+      const double gr0 = sh.G2[row], gr1 = sh.G2[WS + row];
+      c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
+      c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
+    }
+    const double dg = sh.ldiag[row];
+    constexpr int C = T3 < CH3 ? T3 : CH3;
 #pragma unroll 1
-      for (int t0 = 0; t0 < CPL; t0 += C) {
-        double acc[C];
+    for (int t0 = 0; t0 < T3; t0 += C) {
+      double acc[C];
 #pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int col = g + RG * (t0 + u);
-          double v = 0.0;
-          if (col < ncol) {
-            const double a = coef_a<NQ>(col, dt);
-            double sacc = 0.0;
-            if (a != 0.0) sacc = a * sh.Jt[row * NX + coef_b<NQ>(col)];
+      for (int u = 0; u < C; ++u) {
+        const int col = g + RG * (t0 + u);
+        const double a = coef_a<NQ>(col, dt);
+        const double jb = sh.Jt[row * NX + coef_b<NQ>(col)];
+        double sacc = a != 0.0 ? a * jb : 0.0;
 #pragma unroll
-            for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * NR + col];
-            double base = 0.0;
-            if (row == col) base = row < NX ? sh.lxx[row] : sh.luu[row - NX];
-            double e2 = 0.0;
-            if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[NR + col];
-            v = (base + e2) + sacc;
-            if (row == col) v += 1.0 * reg;
-          }
-          acc[u] = v;
-        }
+        for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * WS + col];
+        const double base = row == col ? dg : 0.0;
+        double e2 = 0.0;
+        if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[WS + col];
+        double v = (base + e2) + sacc;
+        if (row == col) v += 1.0 * reg;
+        acc[u] = v;
+      }
 #pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int col = g + RG * (t0 + u);
-          if (col < ncol) sh.Q[row * NR + col] = acc[u];
-        }
+      for (int u = 0; u < C; ++u) {
+        const int col = g + RG * (t0 + u);
+        if (t0 + u < T3 && g < RG) sh.Q[row * QS + col] = acc[u];
       }
     }
   }
   __syncthreads();
-  // R4: PSD test of Quu - 1e-9 I (every lane, registers, static indices), then the
-  // adjugate of Quu spread over lanes 0..15 (one 3x3 minor each)
+  BWS_TMARK(sh, lane, 2);
+  // R45: PSD test of Quu - 1e-9 I (every lane, registers, static indices); adjugate of Quu
+  // spread over lanes 0..15 (one 3x3 minor each) and broadcast back with readlane (no LDS
+  // round trip); then, in the same round, tq = Qux' Quu_inv, K = -tq', du, dV and
+  // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
+  double q0[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) q0[c] = sh.Q[NX * QS + NX + c];
+  double adj = 0.0;
   {
-    double A[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        A[i * 4 + c] = sh.Q[(NX + i) * NR + NX + c] - (i == c ? 1.0 * eps9 : 0.0);
-    if (!ldlt_is_positive4(A)) return false;
-  }
-  if (lane < 16) {
-    // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
-    const int i = lane >> 2, j = lane & 3;
+    // issue the lane's minor loads before the (branchy) LDLT so their latency overlaps it
+    const int i = (lane >> 2) & 3, j = lane & 3;
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
-    const double* q = &sh.Q[NX * NR + NX];
-#define QM(r, c) q[(r) * NR + (c)]
-    const double det3 = QM(r0, c0) * (QM(r1, c1) * QM(r2, c2) - QM(r1, c2) * QM(r2, c1)) -
-                        QM(r0, c1) * (QM(r1, c0) * QM(r2, c2) - QM(r1, c2) * QM(r2, c0)) +
-                        QM(r0, c2) * (QM(r1, c0) * QM(r2, c1) - QM(r1, c1) * QM(r2, c0));
+    const double* q = &sh.Q[NX * QS + NX];
+#define QM(r, c) q[(r) * QS + (c)]
+    const double m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
+    const double m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
+    const double m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
 #undef QM
-    sh.inv[lane] = ((i + j) & 1) ? -det3 : det3;
+    double A[16];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        A[a * 4 + c] = sh.Q[(NX + a) * QS + NX + c] - (a == c ? 1.0 * eps9 : 0.0);
+    if (!ldlt_is_positive4(A)) return false;
+    // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
+    const double det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
+                        m02 * (m10 * m21 - m11 * m20);
+    adj = ((i + j) & 1) ? -det3 : det3;
   }
-  __syncthreads();
-  if (lane < 16) {
-    const double* q = &sh.Q[NX * NR + NX];
-    const double det = q[0] * sh.inv[0] + q[1] * sh.inv[4] + q[2] * sh.inv[8] + q[3] * sh.inv[12];
-    const int t = ((lane & 3) << 2) | (lane >> 2);
-    const double a = sh.inv[lane] / det, at = sh.inv[t] / det;
-    sh.Qi[lane] = (a + at) / 2;  // Quu_inv = (inv + inv')/2
-    sh.tq[4 * NX + lane] = a;    // unsymmetrised inverse, for dV
-  }
-  __syncthreads();
-  // R4b: K = -Quu_inv Qux, tq = Qux' Quu_inv, du = -Quu_inv Qu, dV = -Qu' Quu^-1 Qu
-  if (lane == 63) {
+  const double det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
+                     q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
+  const double invl = adj / det;
+  double Qi[16];
+  {
+    double inv[16];  // unsymmetrised inverse (uniform)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) inv[e] = lane_bcast(invl, e);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Qi[a * 4 + c] = (inv[a * 4 + c] + inv[c * 4 + a]) / 2;
+    // dV += -Qu' inv Qu, unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
     double s = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       double t = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t += sh.Qv[NX + k] * sh.tq[4 * NX + k * 4 + c];
-      s += t * sh.Qv[NX + c];
+      for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
+      s += t * sh.Q[(NX + c) * QS + QV];
     }
-    sh.dV += -s;  // unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
+    if (lane == 63) sh.dV += -s;
   }
-  __syncthreads();
-  #pragma unroll 1
-  for (int e = lane; e < 8 * NX + 4; e += 64) {
-    if (e < 4 * NX) {
-      const int c = e / NX, j = e - c * NX;
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += -sh.Qi[c * 4 + k] * sh.Q[(NX + k) * NR + j];
-      Kout[c * NX + j] = s;
-    } else if (e < 8 * NX) {
-      const int q = e - 4 * NX, i = q >> 2, c = q & 3;
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += sh.Q[(NX + k) * NR + i] * sh.Qi[k * 4 + c];
-      sh.tq[q] = s;
-    } else {
-      const int c = e - 8 * NX;
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += -sh.Qi[c * 4 + k] * sh.Qv[NX + k];
-      duout[c] = s;
-    }
-  }
-  __syncthreads();
-  // R5: H = sym(Qxx) - tq Qux ; G = Qx - tq Qu.  Lane = (column j, row group): the column
-  // Qux[., j] stays in registers, up to 4 independent row chains per lane.
   {
-    constexpr int G5 = 56 / NX;               // 4 for NX = 14, 9 for NX = 6
-    constexpr int R5 = (NX + G5 - 1) / G5;
-    if (lane < G5 * NX) {
-      const int j = lane % NX, g = lane / NX;
-      double qc[4];
+    // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
+    // of the update for G.  tq row i in registers; K[c][i] = -tq[i][c] exactly (Qi is
+    // symmetric and the sums run in the same order).
+    constexpr int NI = NX + 1, GC = 64 / NI, T5 = (NX + 1 + GC - 1) / GC;
+    const int i = lane % NI, g = lane / NI;
+    const int si = i < NX ? i : QV;
+    double qi[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) qc[c] = sh.Q[(NX + c) * NR + j];
-      constexpr int C = R5 < CH5 ? R5 : CH5;
+    for (int k = 0; k < 4; ++k) qi[k] = sh.Q[(NX + k) * QS + si];
+    double tq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double t = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
+      tq[c] = t;
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *(i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) = -tq[c];
+    }
+    constexpr int C = T5 < CH5 ? T5 : CH5;
 #pragma unroll 1
-      for (int t0 = 0; t0 < R5; t0 += C) {
-        double acc[C];
+    for (int t0 = 0; t0 < T5; t0 += C) {
+      double acc[C];
 #pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int i = g + G5 * (t0 + u);
-          double v = 0.0;
-          if (i < NX) {
-            double sacc = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) sacc += sh.tq[i * 4 + c] * qc[c];
-            v = (sh.Q[i * NR + j] + sh.Q[j * NR + i]) / 2 - sacc;
-          }
-          acc[u] = v;
-        }
-#pragma unroll
-        for (int u = 0; u < C; ++u) {
-          const int i = g + G5 * (t0 + u);
-          if (i < NX) sh.H[i * NX + j] = acc[u];
-        }
-      }
-    } else {
-      for (int i = lane - G5 * NX; i < NX; i += 64 - G5 * NX) {
+      for (int u = 0; u < C; ++u) {
+        const int j = g + GC * (t0 + u);
+        const int sj = j < NX ? j : QV;
         double sacc = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) sacc += sh.tq[i * 4 + c] * sh.Qv[NX + c];
-        const double gi = sh.Qv[i] - sacc;
-        sh.G[i] = gi;
-        Gout[i] = gi;
+        for (int c = 0; c < 4; ++c) sacc += tq[c] * sh.Q[(NX + c) * QS + sj];
+        const double qij = sh.Q[i * QS + sj];
+        const double qji = sh.Q[(j < NX ? j : 0) * QS + i];
+        const double base = j < NX ? (qij + qji) / 2 : qij;
+        acc[u] = base - sacc;
+      }
+#pragma unroll
+      for (int u = 0; u < C; ++u) {
+        const int j = g + GC * (t0 + u);
+        if (t0 + u < T5 && g < GC && i < NX && j <= NX)
+          *(j < NX ? &sh.H[i * NX + j] : &sh.G[i]) = acc[u];
       }
     }
   }
   __syncthreads();
+  BWS_TMARK(sh, lane, 7);
   return true;
 }
 
 // Running-cost derivatives of a WB knot: lx / lxx per state lane (CostBase.cpp:28-31),
 // the control / force part comes precomputed with the partials record (see mhpc_solver.h).
-__device__ __forceinline__ void wb_cost_x(BwsLds& sh, int lane, const SolveParams& sp, double dt,
-                                          double pos) {
+// The lane's weight and fixed reference are loaded once per phase (wb_cost_x_consts): a
+// lane-indexed __constant__ read inside the knot loop is a vector memory load whose wait
+// would also drain the knot's prefetch and stores.
+struct CostXConsts {
+  double w2;   // 2 dt Q[i]
+  double rx;   // reference of state i (unused for i = 0: the position reference)
+};
+__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, double dt) {
+  CostXConsts c{0.0, 0.0};
   if (lane < 14) {
     const int i = lane;
-    const double rxi = i == 0 ? pos : i == 1 ? sp.height : i == 2 ? 0.0
-                       : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : 0.0;
-    sh.l[i] = (2 * dt * cQwb[i]) * (sh.xb[i] - rxi);
-    sh.lxx[i] = 2 * dt * cQwb[i];
+    c.rx = i == 1 ? sp.height : i == 2 ? 0.0 : (i >= 3 && i < 7) ? cQjointBias[i - 3]
+           : i == 7 ? sp.vel : 0.0;
+    c.w2 = 2 * dt * cQwb[i];
+  }
+  return c;
+}
+__device__ __forceinline__ void wb_cost_x(BwsLds& sh, int lane, const CostXConsts& c, double pos) {
+  if (lane < 14) {
+    const double rxi = lane == 0 ? pos : c.rx;
+    sh.l[lane] = c.w2 * (sh.xb[lane] - rxi);
+    sh.ldiag[lane] = c.w2;
   }
 }
 
@@ -568,15 +585,36 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
   __syncthreads();
 }
 
+// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
+constexpr int kVmcnt0 = 0x0F70;
+
+// Store the staged K / du / G of knot record `rec`.  All global traffic of a knot (these
+// stores and the prefetch loads of the next record) is issued back to back right after the
+// wait for the previous prefetch, so the next wait (a full knot later) finds both retired:
+// gfx950 keeps one in-order VM counter for loads and stores.
+template <int NX>
+__device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const BwsLds& sh,
+                                           int lane) {
+#pragma unroll
+  for (int t = 0; t < (5 * NX + 4 + 63) / 64; ++t) {
+    const int e = lane + 64 * t;
+    if (e < 4 * NX) d.K[rec * 56 + e] = sh.Kst[e];
+    else if (e < 4 * NX + 4) d.du[rec * 4 + e - 4 * NX] = sh.dust[e - 4 * NX];
+    else if (e < 5 * NX + 4) d.G[rec * 14 + e - 4 * NX - 4] = sh.G[e - 4 * NX - 4];
+  }
+}
+
 // Backward sweep of one WB phase: knots N-2..0 with a one-knot register prefetch.
+// STANCE: a stance phase (modes 1, 3) carries the contact-force outputs y (C, D, ly, lyy);
+// one loop per variant keeps each variant's hoisted lane addresses out of the other's.
+template <bool STANCE>
 __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
                                BwsLds& sh, int lane, int p, double reg, int64_t* knots) {
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+  const int N = sp.N[p], ko = sp.ko[p];
   const double dt = sp.dt[p];
   const int nom = st->nom_slot;
-  const bool stance = mode == 1 || mode == 3;
+  constexpr bool stance = STANCE;
   const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-  constexpr int NR = 18;
   // prefetch registers: 3 doubles of the partials record + 1 of the nominal knot
   double pre[3], prex = 0;
   auto load = [&](int k) {
@@ -584,25 +622,30 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
 #pragma unroll
     for (int t = 0; t < 3; ++t) {  // 3 x 64 lanes >= PS = 176
       const int e = lane + 64 * t;
-      pre[t] = e < PS ? prec[e] : 0.0;
+      pre[t] = prec[e < PS ? e : PS - 1];  // unconditional: no exec-masked load
     }
-    if (lane < 22) prex = traj_ptr(sp, d, b, nom, ko + k)[lane];
+    const double* tk = traj_ptr(sp, d, b, nom, ko + k);
+    prex = *(lane < 22 ? tk + lane : lane == 22 ? pos + k : tk);
   };
+  const CostXConsts cx = wb_cost_x_consts(lane, sp, dt);
   load(N - 2);
   for (int k = N - 2; k >= 0; --k) {
     const int kk = ko + k;
+    // one explicit wait for the prefetch issued a knot ago (and the stores before it), so
+    // no exec-masked use below leaves them "possibly outstanding" for the compiler
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
     // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D]
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int e = lane + 64 * t;
       if (e < PS_JAC) {
         const int col = e / 9, r = e - col * 9;
-        if (r < 7) sh.W[r * NR + col] = (col == 7 + r ? 1.0 : 0.0) + pre[t] * dt;
-        else if (stance) sh.G2[(r - 7) * NR + col] = pre[t];
+        if (r < 7) sh.W[r * WS + col] = (col == 7 + r ? 1.0 : 0.0) + pre[t] * dt;
+        else if (stance) sh.G2[(r - 7) * WS + col] = pre[t];
       } else if (e < PS) {
         const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
         if (q < 4) sh.l[14 + q] = pre[t];
-        else if (q < 8) sh.luu[q - 4] = pre[t];
+        else if (q < 8) sh.ldiag[14 + q - 4] = pre[t];
         else if (q < 10) sh.ly2[q - 8] = pre[t];
         else sh.lyy2[q - 10] = pre[t];
       }
@@ -610,19 +653,19 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     if (lane < 14) sh.xb[lane] = prex;
     else if (lane < 18) sh.ub[lane - 14] = prex;
     else if (lane < 22) sh.yb[lane - 18] = prex;
+    else if (lane == 22) sh.posk = prex;
     __syncthreads();
+    BWS_TMARK(sh, lane, 8);
+    if (k < N - 2) flush_knot<14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
     if (k > 0) load(k - 1);
-    wb_cost_x(sh, lane, sp, dt, pos[k]);
+    wb_cost_x(sh, lane, cx, sh.posk);
     __syncthreads();
-    double* Kout = d.K + ((size_t)b * sp.NK + kk) * 56;
-    double* duout = d.du + ((size_t)b * sp.NK + kk) * 4;
-    double* Gout = d.G + ((size_t)b * sp.NK + kk) * 14;
-    const bool ok = stance
-                        ? riccati_knot<7, true>(sh, lane, dt, reg, sp.eps9, Kout, duout, Gout)
-                        : riccati_knot<7, false>(sh, lane, dt, reg, sp.eps9, Kout, duout, Gout);
+    BWS_TMARK(sh, lane, 9);
+    const bool ok = riccati_knot<7, STANCE>(sh, lane, dt, reg, sp.eps9);
     ++*knots;
     if (!ok) return false;
   }
+  if (N >= 2) flush_knot<14>(d, (size_t)b * sp.NK + ko, sh, lane);
   return true;
 }
 
@@ -632,41 +675,55 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
   const double dt = sp.dt[p];
   const int nom = st->nom_slot;
   const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-  constexpr int NR = 10;
   double foot[4], cs[2];
   plan_foothold(traj_ptr(sp, d, b, nom, ko), dt * N, mode, foot);
   srb_contact(mode, cs);
   const int m = mode - 1;
-  double prex = 0;
-  if (lane < 10) prex = traj_ptr(sp, d, b, nom, ko + N - 2)[lane];
+  // per-lane cost weight 2 dt Q (lanes 30..35: state i) / 2 dt R (lanes 36..39: control c)
+  // and fixed reference, hoisted out of the knot loop (see wb_cost_x_consts)
+  double fb_w2 = 0.0, fb_rx = 0.0;
+  if (lane >= 30 && lane < 36) {
+    const int i = lane - 30;
+    fb_w2 = 2 * dt * cQfb[i];
+    fb_rx = i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
+  } else if (lane >= 36 && lane < 40) {
+    const int c = lane - 36;
+    fb_w2 = 2 * dt * cRfb[m][c];
+    fb_rx = (c == 1 || c == 3) ? 8.252 * 9.81 : 0.0;
+  }
+  auto loadx = [&](int k) {  // unconditional single load per lane (no exec-masked load)
+    const double* tk = traj_ptr(sp, d, b, nom, ko + k);
+    return *(lane < 10 ? tk + lane : lane == 10 ? pos + k : tk);
+  };
+  double prex = loadx(N - 2);
   for (int k = N - 2; k >= 0; --k) {
     const int kk = ko + k;
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
     if (lane < 6) sh.xb[lane] = prex;
     else if (lane < 10) sh.ub[lane - 6] = prex;
+    else if (lane == 10) sh.posk = prex;
     __syncthreads();
-    if (k > 0 && lane < 10) prex = traj_ptr(sp, d, b, nom, ko + k - 1)[lane];
+    if (k < N - 2) flush_knot<6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+    if (k > 0) prex = loadx(k - 1);
     if (lane < 30) {
       const int r = lane / 10, col = lane - r * 10;
-      sh.W[r * NR + col] = srb_w_entry(r, col, sh.xb, sh.ub, foot, cs, dt);
+      sh.W[r * WS + col] = srb_w_entry(r, col, sh.xb, sh.ub, foot, cs, dt);
     } else if (lane < 36) {
       const int i = lane - 30;
-      const double rxi = i == 0 ? pos[k] : i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
-      sh.l[i] = (2 * dt * cQfb[i]) * (sh.xb[i] - rxi);
-      sh.lxx[i] = 2 * dt * cQfb[i];
+      const double rxi = i == 0 ? sh.posk : fb_rx;
+      sh.l[i] = fb_w2 * (sh.xb[i] - rxi);
+      sh.ldiag[i] = fb_w2;
     } else if (lane < 40) {
       const int c = lane - 36;
-      const double ru = (c == 1 || c == 3) ? 8.252 * 9.81 : 0.0;
-      sh.l[6 + c] = (2 * dt * cRfb[m][c]) * (sh.ub[c] - ru);
-      sh.luu[c] = 2 * dt * cRfb[m][c];
+      sh.l[6 + c] = fb_w2 * (sh.ub[c] - fb_rx);
+      sh.ldiag[6 + c] = fb_w2;
     }
     __syncthreads();
-    double* Kout = d.K + ((size_t)b * sp.NK + kk) * 56;
-    double* duout = d.du + ((size_t)b * sp.NK + kk) * 4;
-    double* Gout = d.G + ((size_t)b * sp.NK + kk) * 14;
-    const bool ok = riccati_knot<3, false>(sh, lane, dt, reg, sp.eps9, Kout, duout, Gout);
+    const bool ok = riccati_knot<3, false>(sh, lane, dt, reg, sp.eps9);
     ++*knots;
     if (!ok) return false;
   }
+  if (N >= 2) flush_knot<6>(d, (size_t)b * sp.NK + ko, sh, lane);
   return true;
 }
 
@@ -694,7 +751,9 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
     bool ok;
     if (wb) {
       terminal_value<14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
-      ok = sweep_wb_phase(sp, d, b, st, sh, lane, p, reg, &kn);
+      const int mode = sp.mode[p];
+      ok = (mode == 1 || mode == 3) ? sweep_wb_phase<true>(sp, d, b, st, sh, lane, p, reg, &kn)
+                                    : sweep_wb_phase<false>(sp, d, b, st, sh, lane, p, reg, &kn);
       *knots_wb += kn;
     } else {
       terminal_value<6>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
@@ -709,7 +768,12 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
   return true;
 }
 
-__global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
+// WAVES: minimum resident waves per SIMD requested from the register allocator.  One wave
+// per problem; while the batch fits one wave per SIMD (B <= 4 x CUs) the 1-wave build (no
+// register cap, widest ILP) is fastest, beyond that the 2-wave build hides latency by
+// co-residency.
+template <int WAVES>
+__global__ __launch_bounds__(64, WAVES) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
   const int b = blockIdx.x;
   if (b >= sp.B) return;
   ProbState* st = &d.st[b];
@@ -719,6 +783,12 @@ __global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double up
   int bws_iter = 1;
   int64_t knots = 0, knots_wb = 0, px_reads = 0, sweeps = 0;
   bool aborted = false;
+#ifdef MHPC_BWS_TIMING
+  if (threadIdx.x < 12) sh.cyc[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sh.tlast = clock64();
+  const unsigned long long t_start = clock64();
+  __syncthreads();
+#endif
   for (;;) {
     ++sweeps;
     if (bws_sweep(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
@@ -727,6 +797,11 @@ __global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double up
     if (reg > 1000) { aborted = true; break; }
   }
   __syncthreads();
+#ifdef MHPC_BWS_TIMING
+  if (threadIdx.x == 0) sh.cyc[0] = clock64() - t_start;
+  __syncthreads();
+  if (threadIdx.x < 12) atomicAdd(&g_bws_cyc[threadIdx.x], sh.cyc[threadIdx.x]);
+#endif
   if (threadIdx.x == 0) {
     st->cnt[C_DDP]++;
     st->cnt[C_BWS] += sweeps;
@@ -752,8 +827,36 @@ __global__ __launch_bounds__(64) void k_bws(SolveParams sp, DevBufs d, double up
 }
 
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, double update_reg, hipStream_t s) {
-  hipLaunchKernelGGL(k_bws, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+#ifdef MHPC_BWS_WAVES
+  hipLaunchKernelGGL(k_bws<MHPC_BWS_WAVES>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+#else
+  if (sp.B <= 4 * ncu)
+    hipLaunchKernelGGL(k_bws<1>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else
+    hipLaunchKernelGGL(k_bws<2>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+#endif
   return hipGetLastError();
 }
 
 }  // namespace mhpc
+
+#ifdef MHPC_BWS_TIMING
+extern "C" int mhpc_dbg_bws_cycles(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mhpc::g_bws_cyc), sizeof(unsigned long long) * 12) !=
+      hipSuccess)
+    return 1;
+  if (reset) {
+    unsigned long long z[12] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mhpc::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

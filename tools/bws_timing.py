@@ -1,0 +1,36 @@
+"""Per-round cycle breakdown of k_bws (needs a -DMHPC_BWS_TIMING build, see
+tools/build_variants.sh): python tools/bws_timing.py <lib.so> [batch]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["MHPC_AMD_LIB"] = sys.argv[1]
+from mhpc_minimal_env_amd import capi, configs, locomotion as L  # noqa: E402
+
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+lib = capi.lib()
+dbg = lib.mhpc_dbg_bws_cycles
+dbg.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+desc = configs.c3_desc()
+loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=B, device=0)
+loco.set_initial_condition(configs.x0_for(desc, B))
+buf = (ctypes.c_ulonglong * 12)()
+for it in range(2):
+    loco.initialization()
+    dbg(buf, 1)
+    loco.solve_mhpc()
+    dbg(buf, 1)
+c = loco.get_counters()
+cyc = np.array(list(buf), dtype=np.float64)
+names = ["total", "R2 (+fb knot load)", "R3", "-", "-", "-", "-", "R45 (psd/inv/K/H/G)",
+         "wb drop (+wait)", "wb cost_x", "", ""]
+knots = c["bws_knots"]
+print("batch", B, "counters", c)
+print(f"{'round':24s} {'cyc/problem':>12s} {'cyc/knot':>10s} {'share':>7s}")
+for i in range(10):
+    print(f"{names[i]:24s} {cyc[i]/B:12.0f} {cyc[i]/knots:10.1f} {cyc[i]/cyc[0]:7.3f}")
+rest = cyc[0] - cyc[1:10].sum()
+print(f"{'other (terminal/impact)':24s} {rest/B:12.0f} {rest/knots:10.1f} {rest/cyc[0]:7.3f}")
