@@ -73,9 +73,15 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
       if (p < sp.n_wb) {
         const double delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
         for (int k = 0; k < N - 1; ++k) {
+#ifdef MHPC_EXP_NOLOAD
+          const double* nk = traj_ptr(sp, d, b, nom, ko);
+          const double* Kk = d.K + ((size_t)b * sp.NK + ko) * 56;
+          const double* duk = d.du + ((size_t)b * sp.NK + ko) * 4;
+#else
           const double* nk = traj_ptr(sp, d, b, nom, ko + k);
           const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
           const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+#endif
           double u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -87,11 +93,13 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
           double xd[14], y[4];
           wb_dynamics<double>(x, u, mode, xd, y);
           V += wb_running_cost(sp, mode, dt, refpos[k], x, u, y, reb, delta, etq, egr);
+#ifndef MHPC_EXP_NOSTORE
           double* ok = traj_ptr(sp, d, b, slot, ko + k);
 #pragma unroll
           for (int i = 0; i < 14; ++i) ok[i] = x[i];
 #pragma unroll
           for (int i = 0; i < 4; ++i) { ok[14 + i] = u[i]; ok[18 + i] = y[i]; }
+#endif
 #pragma unroll
           for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
         }
@@ -289,7 +297,7 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
 // ============================================================================================
 // initialization: references, state, PD warm start (MHPCLocomotion.cpp:47-53,200-215)
 // ============================================================================================
-__global__ void k_init(SolveParams sp, DevBufs d) {
+__global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= sp.B) return;
   const double* x0 = d.x0 + (size_t)b * 14;
@@ -345,11 +353,128 @@ __global__ void k_init(SolveParams sp, DevBufs d) {
     }
     double* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
     for (int i = 0; i < 14; ++i) oe[i] = x[i];
-    if (p + 1 < sp.n_wb && (mode == 2 || mode == 4)) {
-      double xp[14], lam[2];
-      wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
-      for (int i = 0; i < 14; ++i) x[i] = xp[i];
+    // phase transition exactly as the forward sweep does it (MultiPhaseDDP.cpp:351-379)
+    if (p + 1 < sp.P) {
+      if (mode == 2 || mode == 4) {
+        double xp[14], lam[2];
+        wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+        for (int i = 0; i < 14; ++i) x[i] = xp[i];
+      }
+      if (p + 1 >= sp.n_wb) {
+        const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+        x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
+      }
     }
+  }
+  // SRB phases: the reference's first forward_sweep(0) rolls them out with the initial
+  // (zero) controls and zero gains -- u = (0 + 0*0) + sum 0*(x - 0) = +0 exactly -- so the
+  // nominal is completed here and forward_sweep(0) reduces to a cost evaluation (k_cost).
+  if (sp.n_wb == 0)
+    for (int i = 0; i < 6; ++i) x[i] = x0[i];
+  for (int p = sp.n_wb; p < sp.P; ++p) {
+    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const double dt = sp.dt[p];
+    double f[4], s[2];
+    plan_foothold(x, dt * N, mode, f);
+    srb_contact(mode, s);
+    const double u[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < N - 1; ++k) {
+      double xd[6];
+      srb_dynamics(x, u, f, s, xd);
+      double* o = traj_ptr(sp, d, b, 0, ko + k);
+      for (int i = 0; i < 6; ++i) o[i] = x[i];
+      for (int i = 0; i < 4; ++i) { o[6 + i] = u[i]; o[10 + i] = 0.0; }
+      for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
+    }
+    double* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
+    for (int i = 0; i < 6; ++i) oe[i] = x[i];
+  }
+}
+
+// ============================================================================================
+// k_cost: forward_sweep(0) at the top of an AL iteration (MultiPhaseDDP.cpp:172-190).
+// With eps = 0 the rollout reproduces the nominal trajectory bit for bit (u = u_nom + 0 +
+// K * 0 and the same dynamics code on the same state), so only the costs change (new ReB
+// flag, sigma / lambda).  One wave per problem: the running cost of every knot in
+// parallel, then per phase the sum in knot order (the rollout's association), terminal
+// cost, AL term and touchdown constraint.
+// ============================================================================================
+__global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_iter) {
+  const int b = blockIdx.x;
+  if (b >= sp.B) return;
+  ProbState* st = &d.st[b];
+  if (!st->active) return;
+  const int lane = threadIdx.x;
+  __shared__ double sc[MHPC_MAX_KNOTS];
+  __shared__ double sV[MAXP], sH[MAXP];
+  const bool reb_off = (st->viol > 0.05) || al_iter == 1;
+  const bool reb = sp.ReB_active && !reb_off;
+  const int nom = st->nom_slot;
+  const double* refpos = d.refpos + (size_t)b * sp.NK;
+  for (int kk = lane; kk < sp.NK; kk += 64) {
+    int p = 0;
+    while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
+    const int k = kk - sp.ko[p], mode = sp.mode[p];
+    double c = 0.0;
+    if (k < sp.N[p] - 1) {
+      const double* r = traj_ptr(sp, d, b, nom, kk);
+      if (p < sp.n_wb)
+        c = wb_running_cost(sp, mode, sp.dt[p], refpos[kk], r, r + 14, r + 18, reb, st->delta[p],
+                            st->eps_tq[p], st->eps_grf[p]);
+      else
+        c = fb_running_cost(sp, mode, sp.dt[p], refpos[kk], r, r + 6);
+    }
+    sc[kk] = c;
+  }
+  __syncthreads();
+  if (lane < sp.P) {
+    const int p = lane, mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    double V = 0, h = 0;
+    for (int k = 0; k < N - 1; ++k) V += sc[ko + k];
+    const double* x = traj_ptr(sp, d, b, nom, ko + N - 1);
+    if (p < sp.n_wb) {
+      double rx[14];
+      wb_term_ref(sp, mode, refpos[ko + N - 1], rx);
+      double Phi = 0;
+      for (int i = 0; i < 14; ++i) { const double e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+      Phi = Phi * 0.5;
+      if (ntc_of(mode, true)) {
+        h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
+        if (sp.AL_active) {
+          const double s = st->sigma[p], lam = st->lambda[p];
+          const double sh2 = s * h / 2;
+          Phi += 50 * (sh2 * sh2 + lam * h);
+        }
+      }
+      V += Phi;
+    } else {
+      double rx[6];
+      fb_term_ref(sp, refpos[ko + N - 1], rx);
+      double Phi = 0;
+      for (int i = 0; i < 6; ++i) { const double e = x[i] - rx[i]; Phi += e * cQffb[i] * e; }
+      V += Phi * 0.5;
+    }
+    sV[p] = V;
+    sH[p] = h;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    double J = 0, viol2 = 0;
+    for (int p = 0; p < sp.P; ++p) {
+      J += sV[p];
+      viol2 += sH[p] * sH[p];
+      st->V[p] = sV[p];
+      st->h[p] = sH[p];
+    }
+    st->reb_active = reb ? 1 : 0;
+    st->J = J;
+    st->viol = sqrt(viol2);
+    st->al_iter = al_iter;
+    st->reg = 0;
+    st->ddp_active = 1;
+    st->al_partials = 1;
+    st->cnt[C_FWD]++;
+    st->cnt[C_PAR_RUN]++;
   }
 }
 
@@ -427,6 +552,11 @@ hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
   hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d);
   return hipGetLastError();
 }
+hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hipStream_t s) {
+  hipLaunchKernelGGL(k_cost, dim3(sp.B), dim3(64), 0, s, sp, d, al_iter);
+  return hipGetLastError();
+}
+
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int full, int al_iter,
                           int ddp_iter, int max_ddp, hipStream_t s) {
   const int nc = full ? 1 : sp.n_cand;

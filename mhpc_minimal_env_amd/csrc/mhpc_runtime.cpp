@@ -16,6 +16,7 @@ hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
+hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_export(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_reduce_counters(const SolveParams&, const DevBufs&, unsigned long long*,
@@ -47,7 +48,7 @@ int fail(int code, const std::string& msg) {
 }  // namespace
 
 enum { K_INIT = 0, K_FULL, K_LS, K_PAR, K_BWS, K_AL, NKERN };
-static const char* kKernelNames[NKERN] = {"k_init", "k_rollout(full)", "k_rollout(linesearch)",
+static const char* kKernelNames[NKERN] = {"k_init", "k_cost(forward_sweep0)", "k_rollout(linesearch)",
                                           "k_partials", "k_bws", "k_al_end"};
 
 struct mhpc_handle {
@@ -69,13 +70,13 @@ struct mhpc_handle {
   double kms[NKERN] = {}, kbytes[NKERN] = {};
   int64_t klaunch[NKERN] = {};
   // algorithmic byte model per problem
-  double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0;
+  double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0, by_cost = 0;
 };
 
 // Algorithmic HBM bytes (fp64) of one problem for each kernel's unit of work.
 static void byte_model(mhpc_handle* h) {
   const SolveParams& sp = h->sp;
-  double rr = 14 * 8, rw = 0, pb = 0, ib = sp.NK * 8.0;
+  double rr = 14 * 8, rw = 0, pb = 0, ib = sp.NK * 8.0, cb = 0;
   for (int p = 0; p < sp.P; ++p) {
     const bool wb = p < sp.n_wb;
     const int n = wb ? 14 : 6, N = sp.N[p];
@@ -83,6 +84,10 @@ static void byte_model(mhpc_handle* h) {
     rr += (N - 1) * 8.0 * ((n + 4) + 4 * n + 4 + 1) + 8.0;
     // each candidate writes x,u,y of every knot (x only at the last knot)
     rw += (N - 1) * 8.0 * (n + 8) + n * 8.0;
+    // k_cost: nominal x,u(,y) of every knot + refpos
+    cb += (N - 1) * 8.0 * (n + 4 + (wb ? 4 : 0) + 1) + 8.0 * (n + 1);
+    // k_init: x,u,y written for every knot (WB and SRB)
+    if (!wb) ib += N * 8.0 * 14;
     if (wb) {
       const bool imp = sp.mode[p] == 2 || sp.mode[p] == 4;
       pb += (N - 1) * 8.0 * (18 + PS) + (imp ? 8.0 * (14 + 196) : 0.0);
@@ -93,6 +98,7 @@ static void byte_model(mhpc_handle* h) {
   h->by_roll_write = rw;
   h->by_par = pb;
   h->by_init = ib;
+  h->by_cost = cb;
 }
 // backward sweep: per WB knot partials record + x,u,y + refpos read, K,du,G written;
 // per SRB knot x,u + refpos read, K,du,G written; Px read per impact-aware step
@@ -334,7 +340,7 @@ static int solve_async(mhpc_handle* h) {
   int n_al = 0;
   for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
   for (int al = 1; al <= o.max_AL_iter; ++al) {
-    LAUNCH(h, K_FULL, launch_rollout(sp, d, 1, al, 0, 0, h->stream));  // forward_sweep(0)
+    LAUNCH(h, K_FULL, launch_cost(sp, d, al, h->stream));  // forward_sweep(0)
     LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     int max_ddp = 0;
     for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
@@ -369,7 +375,7 @@ extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
   rc = collect_profile(h);
   if (rc) return rc;
   const unsigned long long* c = h->cnt;
-  h->kbytes[K_FULL] += c[C_FWD] * (h->by_roll_read + h->by_roll_write);
+  h->kbytes[K_FULL] += c[C_FWD] * h->by_cost;
   h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read + c[C_LS_RUN] * h->by_roll_write;
   h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
   h->kbytes[K_BWS] += c[C_BWS_KNOTS_WB] * kBwsWbKnot + c[C_BWS_KNOTS_FB] * kBwsFbKnot +
