@@ -131,8 +131,8 @@ int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
 
 /* Per-kernel device timing (HIP events around every launch on the handle's stream) and the
  * algorithmic HBM bytes each kernel must move (model in DESIGN.md §Roofline), accumulated
- * over all solves since the last reset.  Kernel ids: 0 init, 1 rollout_full,
- * 2 rollout_linesearch, 3 partials, 4 backward_sweep, 5 al_update. */
+ * over all solves since the last reset.  Kernel ids: 0 init, 1 forward_sweep(0) cost,
+ * 2 line search (rollouts + costs + selection), 3 partials, 4 backward_sweep, 5 al_update. */
 #define MHPC_NUM_KERNELS 6
 const char* mhpc_kernel_name(int k);
 int mhpc_set_profiling(mhpc_handle* h, int on);

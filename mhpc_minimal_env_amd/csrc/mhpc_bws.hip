@@ -25,12 +25,13 @@ namespace mhpc {
 
 // Padded LDS shapes: every lane of a round runs the same straight-line code; rows / columns
 // past the real extents land in padding that no real output reads.
-constexpr int WS = 20;          // row stride of W / G2 (columns of [A B], padded)
-constexpr int JR = 20;          // rows of Jt (padded)
-constexpr int QR = 20;          // rows of Q (padded)
+// Sized for the 64- and the 128-thread block (see riccati_knot's static_asserts).
+constexpr int WS = 24;          // row stride of W / G2 (columns of [A B], padded)
+constexpr int JR = 24;          // rows of Jt (padded)
+constexpr int QR = 24;          // rows of Q (padded)
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
-  static constexpr int QS = NX == 14 ? 19 : 13;  // row stride of Q; column QV holds Qv
+  static constexpr int QS = NX == 14 ? 22 : 13;  // row stride of Q; column QV holds Qv
   static constexpr int QV = QS - 1;
 };
 
@@ -44,7 +45,7 @@ struct BwsLds {
   union {
     struct {
       double Jt[JR * 14];  // [A B]' H   (NR x NX)
-      double Q[QR * 19];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
+      double Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
     };
     struct {
       double H2[196];      // impact-aware step: lifted H' and (Px' H2)
@@ -119,51 +120,50 @@ __device__ __forceinline__ void inverse4(const double* m, double* inv) {
   for (int i = 0; i < 16; ++i) inv[i] = a[i] / det;
 }
 
-// Symmetric swap of indices K < I of a 4x4 lower triangle, exactly as Eigen's
-// ldlt_inplace<Lower>::unblocked applies a transposition (compile-time indices).
-template <int K, int I>
-__device__ __forceinline__ void ldlt_swap(double* A) {
-#pragma unroll
-  for (int j = 0; j < K; ++j) { const double t = A[K * 4 + j]; A[K * 4 + j] = A[I * 4 + j]; A[I * 4 + j] = t; }
-#pragma unroll
-  for (int i = I + 1; i < 4; ++i) { const double t = A[i * 4 + K]; A[i * 4 + K] = A[i * 4 + I]; A[i * 4 + I] = t; }
-  { const double t = A[K * 4 + K]; A[K * 4 + K] = A[I * 4 + I]; A[I * 4 + I] = t; }
-#pragma unroll
-  for (int i = K + 1; i < I; ++i) { const double t = A[i * 4 + K]; A[i * 4 + K] = A[I * 4 + i]; A[I * 4 + i] = t; }
+// Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209) on the lower triangle:
+// ldlt_inplace<Lower>::unblocked with diagonal pivoting (first largest |diagonal|), the
+// symmetric transposition applied to the lower triangle only, sign bookkeeping from
+// ZeroSign; true iff no strictly negative pivot.  Branch-free (the pivot swaps are
+// selects) so the scheduler can interleave it with the independent inverse / value-
+// function work of the same round; same arithmetic as the oracle.
+__device__ __forceinline__ void sel_swap(bool c, double& a, double& b) {
+  const double ta = a, tb = b;
+  a = c ? tb : ta;
+  b = c ? ta : tb;
 }
-
-template <int K>
-__device__ __forceinline__ void ldlt_pivot(double* A) {
-  int big = K;
-  double bv = fabs(A[K * 4 + K]);
-#pragma unroll
-  for (int i = K + 1; i < 4; ++i)
-    if (fabs(A[i * 4 + i]) > bv) { bv = fabs(A[i * 4 + i]); big = i; }
-  if (K < 1 && big == 1) ldlt_swap<(K < 1 ? K : 0), 1>(A);
-  if (K < 2 && big == 2) ldlt_swap<(K < 2 ? K : 0), 2>(A);
-  if (K < 3 && big == 3) ldlt_swap<(K < 3 ? K : 0), 3>(A);
-}
-
-// Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209): diagonal pivoting,
-// sign bookkeeping from ZeroSign; true iff no strictly negative pivot.
 __device__ __forceinline__ bool ldlt_is_positive4(double* A) {
   int sign = 0;  // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
   bool stop = false;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (stop) continue;
-    if (k == 0) ldlt_pivot<0>(A);
-    else if (k == 1) ldlt_pivot<1>(A);
-    else if (k == 2) ldlt_pivot<2>(A);
-    else ldlt_pivot<3>(A);
+    int big = k;
+    double bv = fabs(A[k * 5]);
+#pragma unroll
+    for (int i = k + 1; i < 4; ++i) {
+      const double v = fabs(A[i * 5]);
+      const bool gt = v > bv;
+      bv = gt ? v : bv;
+      big = gt ? i : big;
+    }
+#pragma unroll
+    for (int I = k + 1; I < 4; ++I) {
+      const bool sw = big == I;
+#pragma unroll
+      for (int j = 0; j < k; ++j) sel_swap(sw, A[k * 4 + j], A[I * 4 + j]);
+#pragma unroll
+      for (int i = I + 1; i < 4; ++i) sel_swap(sw, A[i * 4 + k], A[i * 4 + I]);
+      sel_swap(sw, A[k * 5], A[I * 5]);
+#pragma unroll
+      for (int i = k + 1; i < I; ++i) sel_swap(sw, A[i * 4 + k], A[I * 4 + i]);
+    }
     if (k > 0) {
       double temp[3];
 #pragma unroll
-      for (int j = 0; j < k; ++j) temp[j] = A[j * 4 + j] * A[k * 4 + j];
+      for (int j = 0; j < k; ++j) temp[j] = A[j * 5] * A[k * 4 + j];
       double s = 0;
 #pragma unroll
       for (int j = 0; j < k; ++j) s += A[k * 4 + j] * temp[j];
-      A[k * 4 + k] -= s;
+      A[k * 5] -= s;
 #pragma unroll
       for (int i = k + 1; i < 4; ++i) {
         double t = 0;
@@ -172,16 +172,19 @@ __device__ __forceinline__ bool ldlt_is_positive4(double* A) {
         A[i * 4 + k] -= t;
       }
     }
-    const double akk = A[k * 4 + k];
+    const double akk = A[k * 5];
     const bool valid = fabs(akk) > 0.0;
-    if (k == 0 && !valid) { sign = 0; stop = true; continue; }
-    if (k < 3 && valid) {
+    if (k == 0) stop = !valid;  // whole diagonal zero: ZeroSign, stop
 #pragma unroll
-      for (int i = k + 1; i < 4; ++i) A[i * 4 + k] /= akk;
+    for (int i = k + 1; i < 4; ++i) {
+      const double q = A[i * 4 + k] / akk;
+      A[i * 4 + k] = valid ? q : A[i * 4 + k];
     }
-    if (sign == 1) { if (akk < 0.0) sign = 3; }
-    else if (sign == 2) { if (akk > 0.0) sign = 3; }
-    else if (sign == 0) { if (akk > 0.0) sign = 1; else if (akk < 0.0) sign = 2; }
+    int ns = sign;
+    if (sign == 1) ns = akk < 0.0 ? 3 : 1;
+    else if (sign == 2) ns = akk > 0.0 ? 3 : 2;
+    else if (sign == 0) ns = akk > 0.0 ? 1 : (akk < 0.0 ? 2 : 0);
+    sign = stop ? 0 : ns;
   }
   return sign == 1 || sign == 0;
 }
@@ -217,7 +220,7 @@ __device__ __forceinline__ int coef_b(int col) {
 #endif
 constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
 
-template <int NQ, bool HAS_Y>
+template <int NT, int NQ, bool HAS_Y>
 __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
   constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
@@ -225,7 +228,8 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
   // of [H | G].  Lane = (column j, row group g): the column stays in registers and the lane
   // runs T2 independent row chains.
   {
-    constexpr int NC = NX + 1, GR = 64 / NC, T2 = (NR + GR - 1) / GR;
+    constexpr int NC = NX + 1, GR = NT / NC, T2 = (NR + GR - 1) / GR;
+    static_assert(GR * T2 <= JR && GR * T2 <= QR && GR * T2 <= WS, "R2 padding");
     const int j = lane % NC, g = lane / NC;
     const bool isg = j == NX;
     const double* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
@@ -265,7 +269,8 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
   // (+ reg on the diagonal).  Lane = (row of Jt, column group g), the row Jt[row, NQ..] in
   // registers, T3 independent column chains.
   {
-    constexpr int RG = 64 / NR, T3 = NX == 14 ? 6 : 2;  // columns g + RG t < QV
+    constexpr int RG = NT / NR, T3 = (NR + RG - 1) / RG;  // columns g + RG t < QV
+    static_assert(RG * T3 <= QV && RG * T3 <= WS, "R3 padding");
     const int row = lane % NR, g = lane / NR;
     double jr[NQ];
 #pragma unroll
@@ -313,9 +318,11 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
 #pragma unroll
   for (int c = 0; c < 4; ++c) q0[c] = sh.Q[NX * QS + NX + c];
   double adj = 0.0;
+  bool psd;
   {
-    // issue the lane's minor loads before the (branchy) LDLT so their latency overlaps it
-    const int i = (lane >> 2) & 3, j = lane & 3;
+    // the PSD verdict is applied at the end of the round: a failed knot abandons the sweep
+    // (everything written here is rewritten by the retry), only dV must stay untouched
+    const int i = (lane >> 2) & 3, j = lane & 3;  // lanes 0..15 of every wave
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
     const double* q = &sh.Q[NX * QS + NX];
@@ -330,7 +337,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         A[a * 4 + c] = sh.Q[(NX + a) * QS + NX + c] - (a == c ? 1.0 * eps9 : 0.0);
-    if (!ldlt_is_positive4(A)) return false;
+    psd = ldlt_is_positive4(A);
     // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
     const double det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
                         m02 * (m10 * m21 - m11 * m20);
@@ -357,13 +364,13 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
       for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
       s += t * sh.Q[(NX + c) * QS + QV];
     }
-    if (lane == 63) sh.dV += -s;
+    if (lane == 63 && psd) sh.dV += -s;
   }
   {
     // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
     // of the update for G.  tq row i in registers; K[c][i] = -tq[i][c] exactly (Qi is
     // symmetric and the sums run in the same order).
-    constexpr int NI = NX + 1, GC = 64 / NI, T5 = (NX + 1 + GC - 1) / GC;
+    constexpr int NI = NX + 1, GC = NT / NI, T5 = (NX + 1 + GC - 1) / GC;
     const int i = lane % NI, g = lane / NI;
     const int si = i < NX ? i : QV;
     double qi[4];
@@ -407,7 +414,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
   }
   __syncthreads();
   BWS_TMARK(sh, lane, 7);
-  return true;
+  return psd;
 }
 
 // Running-cost derivatives of a WB knot: lx / lxx per state lane (CostBase.cpp:28-31),
@@ -464,7 +471,7 @@ __device__ __forceinline__ double srb_w_entry(int r, int col, const double* x, c
 // Terminal value function of phase p (SinglePhase.cpp:189-191): G = Phix + Gnext,
 // H = Phixx + Hnext, with Gnext/Hnext in sh.G/sh.H; AL partials only while st->al_partials
 // (quirk B1: forward_sweep_partials_only does not add them).
-template <int NX>
+template <int NT, int NX>
 __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLds& sh, int lane,
                                int p, double pos, const double* xe, double* Gout) {
   constexpr bool wb = NX == 14;
@@ -486,7 +493,7 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
   const double s = st->sigma[p], lam = st->lambda[p];
   const int ih = mode == 2 ? 3 : 5;  // touchdown Hessian block (theta, hip, knee)
   #pragma unroll 1
-  for (int e = lane; e < NX * NX + NX; e += 64) {
+  for (int e = lane; e < NX * NX + NX; e += NT) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
       double v = i == j ? (wb ? cQfwb[mode - 1][i] : cQffb[i]) : 0.0;
@@ -514,6 +521,7 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
 
 // impact_aware_step (MultiPhaseDDP.cpp:300-341) for a WB phase p: sh.G/H hold CTG[0] of
 // phase p+1 (6-dim if that phase is SRB); on exit the 14-dim Gnext/Hnext of phase p.
+template <int NT>
 __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsLds& sh, int lane,
                             int p, int64_t* px_reads) {
   const int mode = sp.mode[p];
@@ -521,7 +529,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
   const bool imp = mode == 2 || mode == 4;
   // lift to the full-model space: E' G', E' H' E (E = _stateProj for an SRB next phase)
   #pragma unroll 1
-  for (int e = lane; e < 196 + 14; e += 64) {
+  for (int e = lane; e < 196 + 14; e += NT) {
     if (e < 196) {
       const int i = e / 14, j = e - i * 14;
       double v;
@@ -546,14 +554,14 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
   if (imp) {
     const double* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
     #pragma unroll 1
-    for (int e = lane; e < 196; e += 64) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
+    for (int e = lane; e < 196; e += NT) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
     if (lane == 0) ++*px_reads;
   }
   __syncthreads();
   if (imp) {
     // G = Px' G2 ; T = Px' H2 ; H = T Px
     #pragma unroll 1
-    for (int e = lane; e < 196 + 14; e += 64) {
+    for (int e = lane; e < 196 + 14; e += NT) {
       if (e < 196) {
         const int i = e / 14, j = e - i * 14;
         double s = 0;
@@ -570,7 +578,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
     }
     __syncthreads();
     #pragma unroll 1
-    for (int e = lane; e < 196; e += 64) {
+    for (int e = lane; e < 196; e += NT) {
       const int i = e / 14, j = e - i * 14;
       double s = 0;
 #pragma unroll
@@ -579,7 +587,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
     }
   } else {
     #pragma unroll 1
-    for (int e = lane; e < 196; e += 64) sh.H[e] = sh.H2[e];
+    for (int e = lane; e < 196; e += NT) sh.H[e] = sh.H2[e];
     if (lane < 14) sh.G[lane] = sh.G2v[lane];
   }
   __syncthreads();
@@ -592,12 +600,12 @@ constexpr int kVmcnt0 = 0x0F70;
 // stores and the prefetch loads of the next record) is issued back to back right after the
 // wait for the previous prefetch, so the next wait (a full knot later) finds both retired:
 // gfx950 keeps one in-order VM counter for loads and stores.
-template <int NX>
+template <int NT, int NX>
 __device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const BwsLds& sh,
                                            int lane) {
 #pragma unroll
-  for (int t = 0; t < (5 * NX + 4 + 63) / 64; ++t) {
-    const int e = lane + 64 * t;
+  for (int t = 0; t < (5 * NX + 4 + NT - 1) / NT; ++t) {
+    const int e = lane + NT * t;
     if (e < 4 * NX) d.K[rec * 56 + e] = sh.Kst[e];
     else if (e < 4 * NX + 4) d.du[rec * 4 + e - 4 * NX] = sh.dust[e - 4 * NX];
     else if (e < 5 * NX + 4) d.G[rec * 14 + e - 4 * NX - 4] = sh.G[e - 4 * NX - 4];
@@ -607,7 +615,7 @@ __device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const B
 // Backward sweep of one WB phase: knots N-2..0 with a one-knot register prefetch.
 // STANCE: a stance phase (modes 1, 3) carries the contact-force outputs y (C, D, ly, lyy);
 // one loop per variant keeps each variant's hoisted lane addresses out of the other's.
-template <bool STANCE>
+template <int NT, bool STANCE>
 __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
                                BwsLds& sh, int lane, int p, double reg, int64_t* knots) {
   const int N = sp.N[p], ko = sp.ko[p];
@@ -615,13 +623,14 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
   const int nom = st->nom_slot;
   constexpr bool stance = STANCE;
   const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-  // prefetch registers: 3 doubles of the partials record + 1 of the nominal knot
-  double pre[3], prex = 0;
+  // prefetch registers: PT doubles of the partials record + 1 of the nominal knot
+  constexpr int PT = (PS + NT - 1) / NT;
+  double pre[PT], prex = 0;
   auto load = [&](int k) {
     const double* prec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {  // 3 x 64 lanes >= PS = 176
-      const int e = lane + 64 * t;
+    for (int t = 0; t < PT; ++t) {
+      const int e = lane + NT * t;
       pre[t] = prec[e < PS ? e : PS - 1];  // unconditional: no exec-masked load
     }
     const double* tk = traj_ptr(sp, d, b, nom, ko + k);
@@ -636,8 +645,8 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D]
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int e = lane + 64 * t;
+    for (int t = 0; t < PT; ++t) {
+      const int e = lane + NT * t;
       if (e < PS_JAC) {
         const int col = e / 9, r = e - col * 9;
         if (r < 7) sh.W[r * WS + col] = (col == 7 + r ? 1.0 : 0.0) + pre[t] * dt;
@@ -656,19 +665,20 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     else if (lane == 22) sh.posk = prex;
     __syncthreads();
     BWS_TMARK(sh, lane, 8);
-    if (k < N - 2) flush_knot<14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+    if (k < N - 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
     if (k > 0) load(k - 1);
     wb_cost_x(sh, lane, cx, sh.posk);
     __syncthreads();
     BWS_TMARK(sh, lane, 9);
-    const bool ok = riccati_knot<7, STANCE>(sh, lane, dt, reg, sp.eps9);
+    const bool ok = riccati_knot<NT, 7, STANCE>(sh, lane, dt, reg, sp.eps9);
     ++*knots;
     if (!ok) return false;
   }
-  if (N >= 2) flush_knot<14>(d, (size_t)b * sp.NK + ko, sh, lane);
+  if (N >= 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + ko, sh, lane);
   return true;
 }
 
+template <int NT>
 __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
                                BwsLds& sh, int lane, int p, double reg, int64_t* knots) {
   const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
@@ -703,7 +713,7 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     else if (lane < 10) sh.ub[lane - 6] = prex;
     else if (lane == 10) sh.posk = prex;
     __syncthreads();
-    if (k < N - 2) flush_knot<6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+    if (k < N - 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
     if (k > 0) prex = loadx(k - 1);
     if (lane < 30) {
       const int r = lane / 10, col = lane - r * 10;
@@ -719,20 +729,21 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
       sh.ldiag[6 + c] = fb_w2;
     }
     __syncthreads();
-    const bool ok = riccati_knot<3, false>(sh, lane, dt, reg, sp.eps9);
+    const bool ok = riccati_knot<NT, 3, false>(sh, lane, dt, reg, sp.eps9);
     ++*knots;
     if (!ok) return false;
   }
-  if (N >= 2) flush_knot<6>(d, (size_t)b * sp.NK + ko, sh, lane);
+  if (N >= 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + ko, sh, lane);
   return true;
 }
 
+template <int NT>
 __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st, BwsLds& sh,
                           double reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads) {
   const int lane = threadIdx.x;
   const int nom = st->nom_slot;
   #pragma unroll 1
-  for (int e = lane; e < 196; e += 64) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
+  for (int e = lane; e < 196; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
   if (lane < 14) sh.G[lane] = 0;
   if (lane == 0) sh.dV = 0;
   __syncthreads();
@@ -740,7 +751,7 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
     const bool wb = p < sp.n_wb;
     const int N = sp.N[p], ko = sp.ko[p];
     if (p + 1 < sp.P) {
-      if (wb) impact_step(sp, d, b, sh, lane, p, px_reads);
+      if (wb) impact_step<NT>(sp, d, b, sh, lane, p, px_reads);
       if (lane == 0) sh.dV = st->dV[p + 1];  // dVnext
     }
     __syncthreads();
@@ -750,14 +761,14 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
     int64_t kn = 0;
     bool ok;
     if (wb) {
-      terminal_value<14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
+      terminal_value<NT, 14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
       const int mode = sp.mode[p];
-      ok = (mode == 1 || mode == 3) ? sweep_wb_phase<true>(sp, d, b, st, sh, lane, p, reg, &kn)
-                                    : sweep_wb_phase<false>(sp, d, b, st, sh, lane, p, reg, &kn);
+      ok = (mode == 1 || mode == 3) ? sweep_wb_phase<NT, true>(sp, d, b, st, sh, lane, p, reg, &kn)
+                                    : sweep_wb_phase<NT, false>(sp, d, b, st, sh, lane, p, reg, &kn);
       *knots_wb += kn;
     } else {
-      terminal_value<6>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
-      ok = sweep_fb_phase(sp, d, b, st, sh, lane, p, reg, &kn);
+      terminal_value<NT, 6>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
+      ok = sweep_fb_phase<NT>(sp, d, b, st, sh, lane, p, reg, &kn);
     }
     *knots += kn;
     __syncthreads();
@@ -772,8 +783,8 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
 // per problem; while the batch fits one wave per SIMD (B <= 4 x CUs) the 1-wave build (no
 // register cap, widest ILP) is fastest, beyond that the 2-wave build hides latency by
 // co-residency.
-template <int WAVES>
-__global__ __launch_bounds__(64, WAVES) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
+template <int NT, int WAVES>
+__global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
   const int b = blockIdx.x;
   if (b >= sp.B) return;
   ProbState* st = &d.st[b];
@@ -791,7 +802,7 @@ __global__ __launch_bounds__(64, WAVES) void k_bws(SolveParams sp, DevBufs d, do
 #endif
   for (;;) {
     ++sweeps;
-    if (bws_sweep(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
+    if (bws_sweep<NT>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
     reg = fmax(reg * update_reg, 1e-03);  // MultiPhaseDDP.cpp:218
     ++bws_iter;
     if (reg > 1000) { aborted = true; break; }
@@ -835,12 +846,13 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, double update_reg
       ncu = 256;
   }
 #ifdef MHPC_BWS_WAVES
-  hipLaunchKernelGGL(k_bws<MHPC_BWS_WAVES>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s, sp,
+                     d, update_reg);
 #else
   if (sp.B <= 4 * ncu)
-    hipLaunchKernelGGL(k_bws<1>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<64, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else
-    hipLaunchKernelGGL(k_bws<2>, dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<64, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
 #endif
   return hipGetLastError();
 }

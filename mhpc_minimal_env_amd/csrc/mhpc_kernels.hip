@@ -25,63 +25,90 @@
 namespace mhpc {
 
 // ============================================================================================
-// k_rollout
+// k_rollout: forward_iteration (MultiPhaseDDP.cpp:130-151) -- every Armijo trial at once.
+// Block = two waves working as a pipeline on the same 64 (problem, candidate) lanes:
+//   wave 0  the serial multi-phase rollout u = (u_nom + eps du) + K (x - x_nom),
+//           x+ = x + dt f(x, u), phase transitions (MultiPhaseDDP.cpp:351-379); each knot's
+//           (x, u, y) goes to a two-deep LDS ring;
+//   wave 1  one knot behind: running cost (summed in knot order, exactly the serial
+//           association), terminal cost / AL / touchdown constraint, and the coalesced store
+//           of every candidate's knot record to its trajectory slot.
+// One barrier per knot hands the ring over; the cost and the scattered stores leave the
+// dynamics chain.  At the end the first accepted trial of each problem is selected in-block.
 // ============================================================================================
-constexpr int RO_MAXP = MAXP;
+constexpr int RING_W = 22;  // doubles per ring record (x 14, u 4, y 4)
 
-__global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int full, int al_iter,
-                                                int ddp_iter, int max_ddp) {
-  const int nc = full ? 1 : sp.n_cand;
+// PIPE = false: the same wave plays both roles (no ring, registers hand over) -- better
+// once the batch fills the chip, when a second wave per block only competes for issue.
+template <bool PIPE>
+__global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, DevBufs d,
+                                                             int al_iter, int ddp_iter,
+                                                             int max_ddp) {
+  const int nc = sp.n_cand;
   const int ppw = 64 / nc;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
+  const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
   const int lp = lane / nc, j = lane - lp * nc;
   const int b = blockIdx.x * ppw + lp;
   const bool in = lp < ppw && b < sp.B;
 
-  __shared__ double sJ[64], sViol[64], sV[64][RO_MAXP], sH[64][RO_MAXP];
-  __shared__ int sAcc[64];
+  __shared__ double ring[PIPE ? 2 : 1][RING_W][64];
+  __shared__ double sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
+  __shared__ int sAny;
 
+  if (t == 0) sAny = 0;
+  __syncthreads();
   bool run = false;
+  int nom = 0, slot = 0;
   ProbState* st = nullptr;
   if (in) {
     st = &d.st[b];
-    run = st->active && (full || st->ddp_active);
-  }
-  int nom = 0, slot = 0;
-  double eps = 0;
-  if (run) {
-    if (full) {
-      // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
-      const bool reb_off = (st->viol > 0.05) || al_iter == 1;
-      st->reb_active = (sp.ReB_active && !reb_off) ? 1 : 0;
-    }
+    run = st->active && st->ddp_active;
     nom = st->nom_slot;
     slot = j < nom ? j : j + 1;
-    eps = full ? 0.0 : sp.eps[j];
   }
+  if (w0 && run) sAny = 1;
+  __syncthreads();
+  if (!sAny) return;  // uniform: no problem of this block is still iterating
+
+  const double eps = run ? sp.eps[j] : 0.0;
   const bool reb = run && st->reb_active;
-  double J = 0, viol2 = 0;
-  if (run) {
-    double x[14];
+  double x[14];
+  if (w0 && run) {
     const double* x0 = d.x0 + (size_t)b * 14;
     for (int i = 0; i < 14; ++i) x[i] = x0[i];
-    for (int p = 0; p < sp.P; ++p) {
-      const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-      const double dt = sp.dt[p];
-      double V = 0, h = 0;
-      const double* refpos = d.refpos + (size_t)b * sp.NK + ko;
-      if (p < sp.n_wb) {
-        const double delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
-        for (int k = 0; k < N - 1; ++k) {
-#ifdef MHPC_EXP_NOLOAD
-          const double* nk = traj_ptr(sp, d, b, nom, ko);
-          const double* Kk = d.K + ((size_t)b * sp.NK + ko) * 56;
-          const double* duk = d.du + ((size_t)b * sp.NK + ko) * 4;
-#else
-          const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-          const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-          const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
-#endif
+  }
+  double J = 0, viol2 = 0;
+  int q = 0;  // ring records handed over so far
+  // wave 1: store the lane's ring record (n doubles, n even) to knot kk of its slot with
+  // 16-byte stores (records are 16-byte aligned: KS * 8 = 192)
+  auto store_rec = [&](const double* r, int n, int kk) {
+    double2* o = reinterpret_cast<double2*>(traj_ptr(sp, d, b, slot, kk));
+#pragma unroll
+    for (int i = 0; i < RING_W / 2; ++i)
+      if (2 * i < n) o[i] = make_double2(r[2 * i], r[2 * i + 1]);
+  };
+  for (int p = 0; p < sp.P; ++p) {
+    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const double dt = sp.dt[p];
+    const bool wb = p < sp.n_wb;
+    const int nx = wb ? 14 : 6, nrec = wb ? RING_W : 14;
+    double V = 0, delta = 0, etq = 0, egr = 0;
+    if (w1 && run && wb) { delta = st->delta[p]; etq = st->eps_tq[p]; egr = st->eps_grf[p]; }
+    double f[4], sc[2];
+    if (w0 && run && !wb) {
+      plan_foothold(x, dt * N, mode, f);
+      srb_contact(mode, sc);
+    }
+    const double* refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
+    for (int k = 0; k < N - 1; ++k, ++q) {
+      const int s = PIPE ? (q & 1) : 0;
+      double rr[RING_W];
+      if (w0 && run) {
+        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        if (wb) {
           double u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -92,54 +119,13 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
           }
           double xd[14], y[4];
           wb_dynamics<double>(x, u, mode, xd, y);
-          V += wb_running_cost(sp, mode, dt, refpos[k], x, u, y, reb, delta, etq, egr);
-#ifndef MHPC_EXP_NOSTORE
-          double* ok = traj_ptr(sp, d, b, slot, ko + k);
 #pragma unroll
-          for (int i = 0; i < 14; ++i) ok[i] = x[i];
+          for (int i = 0; i < 14; ++i) rr[i] = x[i];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { ok[14 + i] = u[i]; ok[18 + i] = y[i]; }
-#endif
+          for (int i = 0; i < 4; ++i) { rr[14 + i] = u[i]; rr[18 + i] = y[i]; }
 #pragma unroll
           for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
-        }
-        double* oe = traj_ptr(sp, d, b, slot, ko + N - 1);
-        for (int i = 0; i < 14; ++i) oe[i] = x[i];
-        // terminal cost, constraint and AL (CostBase.cpp:37-47, SinglePhase.cpp:257-275)
-        double rx[14];
-        wb_term_ref(sp, mode, refpos[N - 1], rx);
-        double Phi = 0;
-        for (int i = 0; i < 14; ++i) { const double e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
-        Phi = Phi * 0.5;
-        if (ntc_of(mode, true)) {
-          h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
-          if (sp.AL_active) {
-            const double s = st->sigma[p], lam = st->lambda[p];
-            const double sh2 = s * h / 2;
-            Phi += 50 * (sh2 * sh2 + lam * h);
-          }
-        }
-        V += Phi;
-        // phase transition (MultiPhaseDDP.cpp:351-379)
-        if (p + 1 < sp.P) {
-          if (mode == 2 || mode == 4) {
-            double xp[14], lam[2];
-            wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
-            for (int i = 0; i < 14; ++i) x[i] = xp[i];
-          }
-          if (p + 1 >= sp.n_wb) {
-            const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
-            x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
-          }
-        }
-      } else {
-        double f[4], s[2];
-        plan_foothold(x, dt * N, mode, f);
-        srb_contact(mode, s);
-        for (int k = 0; k < N - 1; ++k) {
-          const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-          const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-          const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        } else {
           double u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -149,69 +135,121 @@ __global__ __launch_bounds__(64) void k_rollout(SolveParams sp, DevBufs d, int f
             u[i] = (nk[6 + i] + eps * duk[i]) + fb;
           }
           double xd[6];
-          srb_dynamics(x, u, f, s, xd);
-          V += fb_running_cost(sp, mode, dt, refpos[k], x, u);
-          double* ok = traj_ptr(sp, d, b, slot, ko + k);
+          srb_dynamics(x, u, f, sc, xd);
 #pragma unroll
-          for (int i = 0; i < 6; ++i) ok[i] = x[i];
+          for (int i = 0; i < 6; ++i) rr[i] = x[i];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { ok[6 + i] = u[i]; ok[10 + i] = 0.0; }
+          for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = 0.0; }
 #pragma unroll
           for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
         }
-        double* oe = traj_ptr(sp, d, b, slot, ko + N - 1);
-        for (int i = 0; i < 6; ++i) oe[i] = x[i];
-        double rx[6];
-        fb_term_ref(sp, refpos[N - 1], rx);
-        double Phi = 0;
-        for (int i = 0; i < 6; ++i) { const double e = x[i] - rx[i]; Phi += e * cQffb[i] * e; }
-        V += Phi * 0.5;
       }
-      J += V;
-      viol2 += h * h;
-      sV[lane][p] = V;
-      sH[lane][p] = h;
+      if (PIPE && w0 && run) {
+#pragma unroll
+        for (int i = 0; i < RING_W; ++i)
+          if (i < nrec) ring[s][i][lane] = rr[i];
+      }
+      if (PIPE) __syncthreads();
+      if (w1 && run) {
+        double r[RING_W];
+#pragma unroll
+        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[s][i][lane] : rr[i]) : 0.0;
+        V += wb ? wb_running_cost(sp, mode, dt, refpos[k], r, r + 14, r + 18, reb, delta, etq, egr)
+                : fb_running_cost(sp, mode, dt, refpos[k], r, r + 6);
+        store_rec(r, nrec, ko + k);
+      }
     }
+    // terminal state of the phase, then the transition (wave 0)
+    const int s = PIPE ? (q & 1) : 0;
+    ++q;
+    double xe[RING_W];
+    if (w0 && run) {
+#pragma unroll
+      for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? x[i] : 0.0;
+      if (PIPE)
+        for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
+      if (wb && p + 1 < sp.P) {
+        if (mode == 2 || mode == 4) {
+          double xp[14], lam[2];
+          wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+          for (int i = 0; i < 14; ++i) x[i] = xp[i];
+        }
+        if (p + 1 >= sp.n_wb) {
+          const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+          x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
+        }
+      }
+    }
+    if (PIPE) __syncthreads();
+    if (w1) {
+      if (run) {
+        if (PIPE) {
+#pragma unroll
+          for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? ring[s][i][lane] : 0.0;
+        }
+        double h = 0;
+        if (wb) {
+          double rx[14];
+          wb_term_ref(sp, mode, refpos[N - 1], rx);
+          double Phi = 0;
+          for (int i = 0; i < 14; ++i) { const double e = xe[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+          Phi = Phi * 0.5;
+          if (ntc_of(mode, true)) {
+            h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
+            if (sp.AL_active) {
+              const double sg = st->sigma[p], lam = st->lambda[p];
+              const double sh2 = sg * h / 2;
+              Phi += 50 * (sh2 * sh2 + lam * h);
+            }
+          }
+          V += Phi;
+        } else {
+          double rx[6];
+          fb_term_ref(sp, refpos[N - 1], rx);
+          double Phi = 0;
+          for (int i = 0; i < 6; ++i) { const double e = xe[i] - rx[i]; Phi += e * cQffb[i] * e; }
+          V += Phi * 0.5;
+        }
+        J += V;
+        viol2 += h * h;
+        sV[p][lane] = V;
+        sH[p][lane] = h;
+        store_rec(xe, nx, ko + N - 1);
+      }
+    }
+  }
+  if (w1 && run) {
     sJ[lane] = J;
     sViol[lane] = sqrt(viol2);
-    const double cost_prev = st->J;
-    const double rhs = cost_prev + sp.gamma * eps * (1 - eps / 2) * st->dV_exp;
-    sAcc[lane] = full ? 1 : (sJ[lane] <= rhs ? 1 : 0);
   }
   __syncthreads();
-  if (run && j == 0) {
-    int sel = nc - 1, nls = nc + 1;
-    for (int c = 0; c < nc; ++c)
-      if (sAcc[lane + c]) { sel = c; nls = c + 1; break; }
-    const int sl = lane + sel;
+  if (w1 && run && j == 0) {
     const double cost_prev = st->J;
+    int sel = nc - 1, nls = nc + 1;
+    for (int c = 0; c < nc; ++c) {
+      const double e = sp.eps[c];
+      const double rhs = cost_prev + sp.gamma * e * (1 - e / 2) * st->dV_exp;
+      if (sJ[lane + c] <= rhs) { sel = c; nls = c + 1; break; }
+    }
+    const int sl = lane + sel;
     st->J = sJ[sl];
     st->viol = sViol[sl];
-    for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[sl][p]; st->h[p] = sH[sl][p]; }
+    for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][sl]; st->h[p] = sH[p][sl]; }
     st->nom_slot = sel < nom ? sel : sel + 1;
-    if (full) {
-      st->al_iter = al_iter;
-      st->reg = 0;
-      st->ddp_active = 1;
-      st->al_partials = 1;
-      st->cnt[C_FWD]++;
-      st->cnt[C_PAR_RUN]++;
+    const bool conv = cost_prev - st->J < sp.DDP_thresh;
+    if (st->ntrace < TRACE)
+      st->trace[st->ntrace++] = (al_iter << 24) | (st->reb_active << 23) | ((conv ? 1 : 0) << 22) |
+                                ((nls & 0xff) << 8) | (st->bws_iter & 0xff);
+    st->cnt[C_LS] += nls < nc ? nls : nc;
+    st->cnt[C_LS_RUN] += nc;
+    st->cnt[C_LS_LAUNCH]++;
+    if (conv) {
+      st->ddp_active = 0;
     } else {
-      const bool conv = cost_prev - st->J < sp.DDP_thresh;
-      if (st->ntrace < TRACE)
-        st->trace[st->ntrace++] = (al_iter << 24) | (st->reb_active << 23) | ((conv ? 1 : 0) << 22) |
-                                  ((nls & 0xff) << 8) | (st->bws_iter & 0xff);
-      st->cnt[C_LS] += nls < nc ? nls : nc;
-      st->cnt[C_LS_RUN] += nc;
-      st->cnt[C_LS_LAUNCH]++;
-      if (conv) {
-        st->ddp_active = 0;
-      } else {
-        st->cnt[C_PAR]++;
-        st->al_partials = 0;
-        if (ddp_iter < max_ddp) st->cnt[C_PAR_RUN]++;
-        else st->ddp_active = 0;
-      }
+      st->cnt[C_PAR]++;
+      st->al_partials = 0;
+      if (ddp_iter < max_ddp) st->cnt[C_PAR_RUN]++;
+      else st->ddp_active = 0;
     }
   }
 }
@@ -557,12 +595,29 @@ hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hip
   return hipGetLastError();
 }
 
-hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int full, int al_iter,
-                          int ddp_iter, int max_ddp, hipStream_t s) {
-  const int nc = full ? 1 : sp.n_cand;
-  const int ppw = 64 / nc;
-  hipLaunchKernelGGL(k_rollout, dim3((sp.B + ppw - 1) / ppw), dim3(64), 0, s, sp, d, full,
-                     al_iter, ddp_iter, max_ddp);
+hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
+                          int max_ddp, hipStream_t s) {
+  const int ppw = 64 / sp.n_cand;
+  const int nblk = (sp.B + ppw - 1) / ppw;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+#ifdef MHPC_RO_PIPE
+  const bool pipe = MHPC_RO_PIPE;
+#else
+  const bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
+                                     // wave per block only competes for issue slots
+#endif
+  if (pipe)
+    hipLaunchKernelGGL(k_rollout<true>, dim3(nblk), dim3(128), 0, s, sp, d, al_iter, ddp_iter,
+                       max_ddp);
+  else
+    hipLaunchKernelGGL(k_rollout<false>, dim3(nblk), dim3(64), 0, s, sp, d, al_iter, ddp_iter,
+                       max_ddp);
   return hipGetLastError();
 }
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
@@ -603,3 +658,5 @@ hipError_t launch_eval_srb(int n, const double* x, const double* u, const double
 }
 
 }  // namespace mhpc
+
+

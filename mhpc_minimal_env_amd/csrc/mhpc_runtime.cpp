@@ -13,7 +13,7 @@
 
 namespace mhpc {
 hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
-hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
+hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, hipStream_t);
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
@@ -80,8 +80,9 @@ static void byte_model(mhpc_handle* h) {
   for (int p = 0; p < sp.P; ++p) {
     const bool wb = p < sp.n_wb;
     const int n = wb ? 14 : 6, N = sp.N[p];
-    // nominal x,u (n+4) + K (4n) + du (4) + refpos read once per problem
-    rr += (N - 1) * 8.0 * ((n + 4) + 4 * n + 4 + 1) + 8.0;
+    // nominal x,u (n+4) + K (4n) + du (4) read once per problem (the candidates of a
+    // problem share them)
+    rr += (N - 1) * 8.0 * ((n + 4) + 4 * n + 4);
     // each candidate writes x,u,y of every knot (x only at the last knot)
     rw += (N - 1) * 8.0 * (n + 8) + n * 8.0;
     // k_cost: nominal x,u(,y) of every knot + refpos
@@ -346,7 +347,7 @@ static int solve_async(mhpc_handle* h) {
     for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
     for (int ddp = 1; ddp <= max_ddp; ++ddp) {
       LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, h->stream));
-      LAUNCH(h, K_LS, launch_rollout(sp, d, 0, al, ddp, max_ddp, h->stream));  // forward_iteration
+      LAUNCH(h, K_LS, launch_rollout(sp, d, al, ddp, max_ddp, h->stream));  // forward_iteration
       if (ddp < max_ddp) LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     }
     LAUNCH(h, K_AL, launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
