@@ -220,8 +220,13 @@ __device__ __forceinline__ int coef_b(int col) {
 #endif
 constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
 
-template <int NT, int NQ, bool HAS_Y>
-__device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9) {
+// r2x / r45x: the caller's per-knot side work, run inside the R2 and R45 rounds (before
+// their barriers) so it needs no round of its own -- global traffic of the knot pipeline
+// (stores of the previous knot, prefetch of the next) and the drop of the next knot's
+// derivatives into LDS (nothing of R45 reads those arrays).
+template <int NT, int NQ, bool HAS_Y, class R2X, class R45X>
+__device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9, R2X&& r2x,
+                             R45X&& r45x) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
   constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
   // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly, G taken as column NX
@@ -263,6 +268,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
       }
     }
   }
+  r2x();
   __syncthreads();
   BWS_TMARK(sh, lane, 1);
   // R3: Qxx = (lxx + C'lyy C) + A'HA ; Qux = (0 + D'lyy C) + B'HA ; Quu = (luu + D'lyy D) + B'HB
@@ -412,6 +418,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
       }
     }
   }
+  r45x();
   __syncthreads();
   BWS_TMARK(sh, lane, 7);
   return psd;
@@ -637,13 +644,11 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     prex = *(lane < 22 ? tk + lane : lane == 22 ? pos + k : tk);
   };
   const CostXConsts cx = wb_cost_x_consts(lane, sp, dt);
-  load(N - 2);
-  for (int k = N - 2; k >= 0; --k) {
-    const int kk = ko + k;
-    // one explicit wait for the prefetch issued a knot ago (and the stores before it), so
-    // no exec-masked use below leaves them "possibly outstanding" for the compiler
-    __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D]
+  // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D],
+  // the control / force cost derivatives, and lx / lxx from the nominal state in prex
+  // (CostBase.cpp:28-31; lane 22 holds the position reference)
+  auto drop = [&]() {
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);  // the prefetch (and the stores issued before it)
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int e = lane + NT * t;
@@ -659,18 +664,26 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
         else sh.lyy2[q - 10] = pre[t];
       }
     }
-    if (lane < 14) sh.xb[lane] = prex;
-    else if (lane < 18) sh.ub[lane - 14] = prex;
-    else if (lane < 22) sh.yb[lane - 18] = prex;
-    else if (lane == 22) sh.posk = prex;
-    __syncthreads();
-    BWS_TMARK(sh, lane, 8);
-    if (k < N - 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
-    if (k > 0) load(k - 1);
-    wb_cost_x(sh, lane, cx, sh.posk);
-    __syncthreads();
-    BWS_TMARK(sh, lane, 9);
-    const bool ok = riccati_knot<NT, 7, STANCE>(sh, lane, dt, reg, sp.eps9);
+    const double pk = lane_bcast(prex, 22);
+    if (lane < 14) {
+      const double rxi = lane == 0 ? pk : cx.rx;
+      sh.l[lane] = cx.w2 * (prex - rxi);
+      sh.ldiag[lane] = cx.w2;
+    }
+  };
+  load(N - 2);
+  drop();
+  __syncthreads();
+  for (int k = N - 2; k >= 0; --k) {
+    const int kk = ko + k;
+    auto r2x = [&]() {
+      if (k < N - 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+      if (k > 0) load(k - 1);
+    };
+    auto r45x = [&]() {
+      if (k > 0) drop();
+    };
+    const bool ok = riccati_knot<NT, 7, STANCE>(sh, lane, dt, reg, sp.eps9, r2x, r45x);
     ++*knots;
     if (!ok) return false;
   }
@@ -705,31 +718,42 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     const double* tk = traj_ptr(sp, d, b, nom, ko + k);
     return *(lane < 10 ? tk + lane : lane == 10 ? pos + k : tk);
   };
-  double prex = loadx(N - 2);
-  for (int k = N - 2; k >= 0; --k) {
-    const int kk = ko + k;
+  // drop of knot k: the nominal (x 6, u 4) and position reference sit in prex of lanes
+  // 0..10; W rows (FBDynamics_par.c order) and the cost derivatives straight from registers
+  auto drop = [&](double px) {
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    if (lane < 6) sh.xb[lane] = prex;
-    else if (lane < 10) sh.ub[lane - 6] = prex;
-    else if (lane == 10) sh.posk = prex;
-    __syncthreads();
-    if (k < N - 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
-    if (k > 0) prex = loadx(k - 1);
+    const double xs[2] = {lane_bcast(px, 0), lane_bcast(px, 1)};
+    const double us[4] = {lane_bcast(px, 6), lane_bcast(px, 7), lane_bcast(px, 8),
+                          lane_bcast(px, 9)};
+    const double pk = lane_bcast(px, 10);
+    const double own = __shfl(px, lane >= 36 ? lane - 30 : (lane >= 30 ? lane - 30 : 0));
     if (lane < 30) {
       const int r = lane / 10, col = lane - r * 10;
-      sh.W[r * WS + col] = srb_w_entry(r, col, sh.xb, sh.ub, foot, cs, dt);
+      sh.W[r * WS + col] = srb_w_entry(r, col, xs, us, foot, cs, dt);
     } else if (lane < 36) {
       const int i = lane - 30;
-      const double rxi = i == 0 ? sh.posk : fb_rx;
-      sh.l[i] = fb_w2 * (sh.xb[i] - rxi);
+      const double rxi = i == 0 ? pk : fb_rx;
+      sh.l[i] = fb_w2 * (own - rxi);
       sh.ldiag[i] = fb_w2;
     } else if (lane < 40) {
       const int c = lane - 36;
-      sh.l[6 + c] = fb_w2 * (sh.ub[c] - fb_rx);
+      sh.l[6 + c] = fb_w2 * (own - fb_rx);
       sh.ldiag[6 + c] = fb_w2;
     }
-    __syncthreads();
-    const bool ok = riccati_knot<NT, 3, false>(sh, lane, dt, reg, sp.eps9);
+  };
+  double prex = loadx(N - 2);
+  drop(prex);
+  __syncthreads();
+  for (int k = N - 2; k >= 0; --k) {
+    const int kk = ko + k;
+    auto r2x = [&]() {
+      if (k < N - 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+      if (k > 0) prex = loadx(k - 1);
+    };
+    auto r45x = [&]() {
+      if (k > 0) drop(prex);
+    };
+    const bool ok = riccati_knot<NT, 3, false>(sh, lane, dt, reg, sp.eps9, r2x, r45x);
     ++*knots;
     if (!ok) return false;
   }
