@@ -50,15 +50,16 @@ def cpu_baseline(desc, opt, sample: int, threads: int):
     }, None
 
 
-def load_pmc(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc(kernel: str, batch: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
+    batch size (profiles/pmc_traffic_b<batch>.json, tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_b{batch}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get("kernels", {}).get(kernel.split("(")[0], {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -69,7 +70,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch-per-gpu", type=int, default=1024)
-    ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -147,7 +148,7 @@ def main():
         roofline = {
             "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_pmc(dom), "alg_bytes_per_launch": bytes_per_launch,
+            "traffic": load_pmc(dom, B), "alg_bytes_per_launch": bytes_per_launch,
             "avg_launch_ms": per_launch_s * 1e3,
         }
         cpu, why = (None, "disabled")

@@ -24,8 +24,6 @@ def load(path, counter):
             name = r["Kernel_Name"]
             m = re.search(r"mhpc::(\w+)", name)
             key = m.group(1) if m else name
-            if key == "k_rollout":  # full sweep (1 lane / problem) vs line search grids
-                key = f"k_rollout[grid={r['Grid_Size']}]"
             acc[key].append(float(r["Counter_Value"]))
     return acc
 
