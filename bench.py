@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def cpu_baseline(desc, opt, sample: int, threads: int):
+def cpu_baseline(desc, opt, sample: int, threads: int, label: str = "C3"):
     """The CPU oracle (restatement of MultiPhaseDDP::solve + the reference's own CasADi
     kernels, oracle/_ref) on the first `sample` problems of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -44,7 +44,7 @@ def cpu_baseline(desc, opt, sample: int, threads: int):
     dt = time.perf_counter() - t0
     return {
         "value": sample / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-        "sample": (f"{sample} C3 problems (same x0 stream), init+solve, CPU restatement of "
+        "sample": (f"{sample} {label} problems (same x0 stream), init+solve, CPU restatement of "
                    f"MultiPhaseDDP::solve calling the reference's own CasADi kernels "
                    f"(oracle/_ref), g++ -O2, {threads} threads, {dt:.2f} s wall"),
     }, None
@@ -64,13 +64,92 @@ def load_pmc(kernel: str, batch: int):
         return None
 
 
+def run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch):
+    """C2: one WB phase (mode 1, N=120); after a solve (untimed setup) every
+    step evaluates 256 trial rollouts (forward_sweep_dynamics_only at the C2 step grid) of
+    each problem's nominal + gains.  value = rollouts/s over all ranks."""
+    from mhpc_minimal_env_amd import configs
+    from mhpc_minimal_env_amd import locomotion as L
+    eps = configs.c2_eps(256)
+    loco = L.MHPCLocomotion(desc=desc, option=opt, batch=B, device=local_rank)
+    loco.set_initial_condition(x0)
+    loco.initialization()
+    loco.solve_mhpc()
+    for _ in range(args.warmup):
+        loco.rollout_costs(eps)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    dev_ms = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dev_ms += loco.rollout_costs(eps)["ms"]
+    barrier()
+    dt = time.perf_counter() - t0
+    tens = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+    if dist is not None:
+        dist.all_reduce(tens, op=dist.ReduceOp.MAX)
+        dt = float(tens[0])
+    if rank == 0:
+        n = world * B * len(eps) * args.steps
+        # algorithmic bytes per launch: nominal x,u + K + du of every knot read once per
+        # problem (the trials share them), J / viol written per trial
+        N = desc.N[0]
+        alg = B * ((N - 1) * 8.0 * (18 + 56 + 4) + 16.0 * len(eps))
+        per_launch_s = dev_ms / 1e3 / args.steps
+        achieved = alg / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+        cpu = {"value": None, "reason": "disabled"}
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            if O.available():
+                ns = min(B, 8)
+                r = O.rollout_costs(desc, opt.to_c(), x0[:ns], eps, nthreads=1)
+                cpu = {"value": ns * len(eps) / r["rollout_cpu_seconds"], "unit": "rollouts/s",
+                       "cores": 1, "kind": "port",
+                       "sample": f"{ns} C2 problems x {len(eps)} step sizes after the same solve, "
+                                 f"oracle forward_sweep_dynamics_only (reference CasADi "
+                                 f"kernels), 1 thread, {r['rollout_cpu_seconds']:.2f} s"}
+            else:
+                cpu = {"value": None, "reason": "oracle/_ref not built on this machine"}
+        line = {
+            "metric": "C2 trial rollouts/sec (1 WB phase N=120, 256 step sizes per nominal)",
+            "value": n / dt, "unit": "rollouts/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (x0 = reference default + splitmix64 perturbation)",
+            "config": {"workload": "C2: WB mode 1, dt=(float)(0.08f/120), N=120; step = 256 "
+                                   "trial rollouts (costs) of every problem's nominal+gains",
+                       "batch_per_gpu": B, "global_batch": world * B,
+                       "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"kernel": "k_eps_rollout", "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": per_launch_s * 1e3},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    loco.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch-per-gpu", type=int, default=1024)
-    ap.add_argument("--cpu-sample", type=int, default=16384)
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="problems per GPU (default: c3 1024, c5 4096, c2 1)")
+    ap.add_argument("--workload", choices=["c3", "c5", "c2"], default="c3",
+                    help="c3: the headline 2WB+2SRB solve (BASELINE configs[2]); c5: 4WB+6SRB "
+                         "bound solve; c2: 256 trial rollouts of one nominal per problem")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="CPU-baseline problems (default: c3 16384, c5 8192)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -91,9 +170,11 @@ def main():
     from mhpc_minimal_env_amd import capi, configs
     from mhpc_minimal_env_amd import locomotion as L
 
-    B = args.batch_per_gpu
-    desc, opt = configs.c3_desc(), L.HSDDP_OPTION()
+    B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c2": 1}[args.workload]
+    desc, opt = getattr(configs, f"{args.workload}_desc")(), L.HSDDP_OPTION()
     x0 = configs.x0_for(desc, B, offset=rank * B)
+    if args.workload == "c2":
+        return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
     loco = L.MHPCLocomotion(desc=desc, option=opt, batch=B, device=local_rank)
     loco.set_initial_condition(x0)
     lib, h = capi.lib(), loco._h
@@ -153,10 +234,13 @@ def main():
         }
         cpu, why = (None, "disabled")
         if world == 1 and not args.no_cpu_baseline:
-            cpu, why = cpu_baseline(desc, opt, args.cpu_sample,
-                                    min(args.cpu_threads, os.cpu_count() or 1))
+            cpu, why = cpu_baseline(desc, opt, args.cpu_sample or
+                                    (16384 if args.workload == "c3" else 8192),
+                                    min(args.cpu_threads, os.cpu_count() or 1),
+                                    label=args.workload.upper())
         line = {
-            "metric": "MHPC solves/sec (2WB+2SRB trot)",
+            "metric": ("MHPC solves/sec (2WB+2SRB trot)" if args.workload == "c3"
+                       else "MHPC solves/sec (4WB+6SRB bound)"),
             "value": total / dt,
             "unit": "solves/s",
             "n_gpus": world,
@@ -169,9 +253,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic (x0 = reference default + splitmix64 perturbation)",
             "config": {
-                "workload": "C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, "
-                            "N=80/phase, HSDDP max_AL=2 max_DDP=3; step = initialization + "
-                            "solve of the whole batch",
+                "workload": (("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, "
+                              "N=80/phase" if args.workload == "c3" else
+                              "C5: Gait() BOUND, 4 WB + 6 SRB, N=80/100 alternating")
+                             + ", HSDDP max_AL=2 max_DDP=3; step = initialization + solve of "
+                               "the whole batch"),
                 "batch_per_gpu": B,
                 "global_batch": world * B,
                 "parallelism": f"batch-sharded x{world}",

@@ -129,6 +129,17 @@ int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, do
                      double* dV_phase, int32_t* trace);
 int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
 
+/* The trial rollouts of MultiPhaseDDP::forward_iteration (MultiPhaseDDP.cpp:130-151, i.e.
+ * SinglePhase::forward_sweep_dynamics_only, SinglePhase.cpp:117-144, chained over phases by
+ * MultiPhaseDDP::forward_sweep_dynamics_only :56-76) at n_eps arbitrary step sizes, from the
+ * handle's current nominal, gains and AL/ReB state (after mhpc_solve, or right after
+ * mhpc_initialize), costs only, nothing modified: J = actual cost, viol = terminal-
+ * constraint violation, both [batch][n_eps].  ms (optional) = device time of the launch.
+ * The C2 workload (256 concurrent rollouts of one nominal). */
+#define MHPC_MAX_ROLLOUT_EPS 4096
+int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, double* J, double* viol,
+                       float* ms);
+
 /* Per-kernel device timing (HIP events around every launch on the handle's stream) and the
  * algorithmic HBM bytes each kernel must move (model in DESIGN.md §Roofline), accumulated
  * over all solves since the last reset.  Kernel ids: 0 init, 1 forward_sweep(0) cost,

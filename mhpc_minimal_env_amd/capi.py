@@ -17,6 +17,7 @@ MHPC_MAX_PHASES = 16
 MHPC_MAX_KNOTS = 1024
 MHPC_TRACE_LEN = 64
 MHPC_NUM_KERNELS = 6
+MHPC_MAX_ROLLOUT_EPS = 4096
 
 MHPC_OK = 0
 MHPC_SOLVE_OK = 0
@@ -113,6 +114,8 @@ SIGNATURES = [
     ("mhpc_get_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP]),
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
+    ("mhpc_rollout_costs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP,
+                                          ctypes.POINTER(ctypes.c_float)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),
     ("mhpc_kernel_name", ctypes.c_char_p, [ctypes.c_int]),
     ("mhpc_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

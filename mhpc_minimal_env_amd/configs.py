@@ -46,3 +46,15 @@ def x0_for(desc, batch: int, offset: int = 0):
     if desc.n_wb == 0:
         x0 = x0[:, L.STATE_PROJ_ROWS]
     return np.ascontiguousarray(x0)
+
+
+def c2_eps(n: int = 256) -> np.ndarray:
+    """C2 step sizes: j = 0..9 the reference's Armijo grid 1, 0.1, 0.1*0.1, ...
+    (parity-pinned), j >= 10 eps = 0.1**(j / 25.5) (deterministic, unpinned)."""
+    j = np.arange(n, dtype=np.float64)
+    eps = np.power(0.1, j / 25.5)
+    e = 1.0
+    for k in range(min(n, 10)):  # eps *= alpha, exactly as forward_iteration steps it
+        eps[k] = e
+        e *= 0.1
+    return eps

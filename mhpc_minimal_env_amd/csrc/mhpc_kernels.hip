@@ -255,6 +255,111 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 }
 
 // ============================================================================================
+// k_eps_rollout: forward_sweep_dynamics_only (SinglePhase.cpp:117-144) at an arbitrary list
+// of step sizes from the current nominal, gains and AL / ReB state, costs only (no stores,
+// no selection): the trial rollouts of forward_iteration without the Armijo stop -- the
+// C2 workload (256 concurrent rollouts of one nominal).  Lane = (problem, step size).
+// ============================================================================================
+__global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, int n_eps,
+                                                    const double* eps_v, double* Jo,
+                                                    double* vo) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)sp.B * n_eps) return;
+  const int b = (int)(t / n_eps), e = (int)(t - (long)b * n_eps);
+  const ProbState* st = &d.st[b];
+  const int nom = st->nom_slot;
+  const double eps = eps_v[e];
+  const bool reb = st->reb_active != 0;
+  double x[14];
+  const double* x0 = d.x0 + (size_t)b * 14;
+  for (int i = 0; i < 14; ++i) x[i] = x0[i];
+  double J = 0, viol2 = 0;
+  for (int p = 0; p < sp.P; ++p) {
+    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const double dt = sp.dt[p];
+    const double* refpos = d.refpos + (size_t)b * sp.NK + ko;
+    double V = 0, h = 0;
+    if (p < sp.n_wb) {
+      const double delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
+      for (int k = 0; k < N - 1; ++k) {
+        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        double u[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double fb = 0;
+#pragma unroll
+          for (int c = 0; c < 14; ++c) fb += Kk[i * 14 + c] * (x[c] - nk[c]);
+          u[i] = (nk[14 + i] + eps * duk[i]) + fb;
+        }
+        double xd[14], y[4];
+        wb_dynamics<double>(x, u, mode, xd, y);
+        V += wb_running_cost(sp, mode, dt, refpos[k], x, u, y, reb, delta, etq, egr);
+#pragma unroll
+        for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
+      }
+      double rx[14];
+      wb_term_ref(sp, mode, refpos[N - 1], rx);
+      double Phi = 0;
+      for (int i = 0; i < 14; ++i) { const double ee = x[i] - rx[i]; Phi += ee * cQfwb[mode - 1][i] * ee; }
+      Phi = Phi * 0.5;
+      if (ntc_of(mode, true)) {
+        h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
+        if (sp.AL_active) {
+          const double sg = st->sigma[p], lam = st->lambda[p];
+          const double sh2 = sg * h / 2;
+          Phi += 50 * (sh2 * sh2 + lam * h);
+        }
+      }
+      V += Phi;
+      if (p + 1 < sp.P) {
+        if (mode == 2 || mode == 4) {
+          double xp[14], lam[2];
+          wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+          for (int i = 0; i < 14; ++i) x[i] = xp[i];
+        }
+        if (p + 1 >= sp.n_wb) {
+          const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+          x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
+        }
+      }
+    } else {
+      double f[4], sc[2];
+      plan_foothold(x, dt * N, mode, f);
+      srb_contact(mode, sc);
+      for (int k = 0; k < N - 1; ++k) {
+        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        double u[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double fb = 0;
+#pragma unroll
+          for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
+          u[i] = (nk[6 + i] + eps * duk[i]) + fb;
+        }
+        double xd[6];
+        srb_dynamics(x, u, f, sc, xd);
+        V += fb_running_cost(sp, mode, dt, refpos[k], x, u);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
+      }
+      double rx[6];
+      fb_term_ref(sp, refpos[N - 1], rx);
+      double Phi = 0;
+      for (int i = 0; i < 6; ++i) { const double ee = x[i] - rx[i]; Phi += ee * cQffb[i] * ee; }
+      V += Phi * 0.5;
+    }
+    J += V;
+    viol2 += h * h;
+  }
+  Jo[t] = J;
+  vo[t] = sqrt(viol2);
+}
+
+// ============================================================================================
 // k_partials: one lane per (problem, knot, tangent direction)
 // ============================================================================================
 __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
@@ -356,7 +461,9 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d) {
     st->eps_grf[p] = 0.01;
   }
   st->status = MHPC_SOLVE_OK;
-  st->active = 1; st->ddp_active = 0; st->reb_active = 0; st->al_partials = 0;
+  // ReB flag as the options set it (what a sweep right after initialization() sees); the
+  // first forward_sweep(0) applies the per-AL-iteration rule (MultiPhaseDDP.cpp:178-183)
+  st->active = 1; st->ddp_active = 0; st->reb_active = sp.ReB_active ? 1 : 0; st->al_partials = 0;
   st->nom_slot = 0; st->al_iter = 0; st->ddp_iter = 0; st->bws_iter = 0; st->ntrace = 0;
   for (int i = 0; i < TRACE; ++i) st->trace[i] = -1;
   for (int i = 0; i < NCNT; ++i) st->cnt[i] = 0;
@@ -618,6 +725,13 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   else
     hipLaunchKernelGGL(k_rollout<false>, dim3(nblk), dim3(64), 0, s, sp, d, al_iter, ddp_iter,
                        max_ddp);
+  return hipGetLastError();
+}
+hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,
+                              const double* eps, double* J, double* viol, hipStream_t s) {
+  const long n = (long)sp.B * n_eps;
+  hipLaunchKernelGGL(k_eps_rollout, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, d, n_eps,
+                     eps, J, viol);
   return hipGetLastError();
 }
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {

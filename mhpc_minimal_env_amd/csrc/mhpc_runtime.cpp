@@ -17,6 +17,8 @@ hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, hip
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
+hipError_t launch_eps_rollout(const SolveParams&, const DevBufs&, int, const double*, double*,
+                              double*, hipStream_t);
 hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_export(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_reduce_counters(const SolveParams&, const DevBufs&, unsigned long long*,
@@ -456,6 +458,38 @@ extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, doubl
     }
     if (trace) memcpy(&trace[(size_t)b * TRACE], st[b].trace, TRACE * sizeof(int32_t));
   }
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, double* J,
+                                  double* viol, float* ms) {
+  if (!h || !eps || !J) return fail(MHPC_ERR_INVALID, "null argument");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+  if (n_eps < 1 || n_eps > MHPC_MAX_ROLLOUT_EPS) return fail(MHPC_ERR_INVALID, "n_eps out of range");
+  HIPCHK(hipSetDevice(h->device));
+  const size_t B = h->sp.B, n = B * (size_t)n_eps;
+  double *deps = nullptr, *dJ = nullptr, *dv = nullptr;
+  auto cleanup = [&]() {
+    if (deps) (void)hipFree(deps);
+    if (dJ) (void)hipFree(dJ);
+    if (dv) (void)hipFree(dv);
+  };
+  hipError_t e = hipMalloc((void**)&deps, n_eps * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dJ, n * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dv, n * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpyAsync(deps, eps, n_eps * sizeof(double), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipEventRecord(h->ev0, h->stream);
+  if (e == hipSuccess) e = launch_eps_rollout(h->sp, h->d, n_eps, deps, dJ, dv, h->stream);
+  if (e == hipSuccess) e = hipEventRecord(h->ev1, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(J, dJ, n * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && viol)
+    e = hipMemcpyAsync(viol, dv, n * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  float t = 0;
+  if (e == hipSuccess) e = hipEventElapsedTime(&t, h->ev0, h->ev1);
+  cleanup();
+  if (e != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("mhpc_rollout_costs: ") + hipGetErrorString(e));
+  if (ms) *ms = t;
   return MHPC_OK;
 }
 

@@ -274,6 +274,19 @@ class MHPCLocomotion:
                    "mhpc_get_counters")
         return {k: getattr(c, k) for k, _ in capi.Counters._fields_}
 
+    def rollout_costs(self, eps) -> dict:
+        """Trial rollouts (forward_sweep_dynamics_only) at every step size in `eps` from the
+        current nominal and gains, costs only: J, viol [batch][len(eps)] and the device ms."""
+        eps = np.ascontiguousarray(eps, dtype=np.float64)
+        J = np.zeros((self.batch, eps.shape[0]))
+        viol = np.zeros_like(J)
+        ms = __import__("ctypes").c_float(0)
+        capi.check(capi.lib().mhpc_rollout_costs(self._h, int(eps.shape[0]), capi.dptr(eps),
+                                                 capi.dptr(J), capi.dptr(viol),
+                                                 __import__("ctypes").byref(ms)),
+                   "mhpc_rollout_costs")
+        return {"J": J, "viol": viol, "ms": ms.value}
+
     def set_profiling(self, on: bool = True):
         capi.check(capi.lib().mhpc_set_profiling(self._h, 1 if on else 0), "mhpc_set_profiling")
 

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <string>
 #include <atomic>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -1120,5 +1121,45 @@ extern "C" int oracle_solve(const mhpc_problem_desc* desc, const mhpc_hsddp_opti
   for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
   worker();
   for (auto& t : th) t.join();
+  return 0;
+}
+
+// forward_sweep_dynamics_only at a list of step sizes from the state a solve leaves behind
+// (nominal, gains, AL / ReB parameters): MultiPhaseDDP::forward_iteration's trial rollouts
+// (MultiPhaseDDP.cpp:130-151) without the Armijo stop, for the C2 rollout workload.
+// J / viol: [batch][n_eps].  do_solve = 0 evaluates right after initialization.
+extern "C" int oracle_rollout_costs(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt,
+                                    int batch, const double* x0, int nthreads, int do_solve,
+                                    int n_eps, const double* eps, double* J, double* viol,
+                                    double* rollout_seconds) {
+  std::atomic<long long> ns(0);
+  if (!g_ref.handle) return 3;
+  const int np = desc->n_wb + desc->n_fb;
+  if (np < 1 || np > MHPC_MAX_PHASES || n_eps < 1) return 1;
+  const int n0 = desc->n_wb > 0 ? 14 : 6;
+  std::atomic<int> next(0);
+  auto worker = [&]() {
+    for (;;) {
+      const int b = next.fetch_add(1);
+      if (b >= batch) break;
+      Problem P;
+      build(P, desc, opt, x0 + (size_t)b * n0);
+      if (do_solve) mp_solve(P);
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int e = 0; e < n_eps; ++e) {
+        mp_forward_sweep(P, eps[e], true);
+        J[(size_t)b * n_eps + e] = P.actual_cost;
+        viol[(size_t)b * n_eps + e] = P.tconstr_violation;
+      }
+      ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                std::chrono::steady_clock::now() - t0).count();
+    }
+  };
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  if (rollout_seconds) *rollout_seconds = ns.load() * 1e-9;  // summed over threads
   return 0;
 }

@@ -85,6 +85,26 @@ def solve(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray, nthread
     return out
 
 
+def rollout_costs(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray, eps,
+                  nthreads: int = 1, do_solve: bool = True) -> dict:
+    """forward_sweep_dynamics_only at every step size in `eps` from the state the solve
+    leaves (oracle_rollout_costs); returns J and viol of shape [batch][len(eps)]."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    eps = np.ascontiguousarray(eps, dtype=np.float64)
+    B, E = x0.shape[0], eps.shape[0]
+    J = np.zeros((B, E))
+    viol = np.zeros((B, E))
+    L = lib()
+    L.oracle_rollout_costs.restype = ctypes.c_int
+    secs = ctypes.c_double(0)
+    rc = L.oracle_rollout_costs(ctypes.byref(desc), ctypes.byref(opt), ctypes.c_int(B), _p(x0),
+                                ctypes.c_int(nthreads), ctypes.c_int(1 if do_solve else 0),
+                                ctypes.c_int(E), _p(eps), _p(J), _p(viol), ctypes.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"oracle_rollout_costs failed ({rc})")
+    return {"J": J, "viol": viol, "rollout_cpu_seconds": secs.value}
+
+
 def decode_trace(t) -> list:
     """Decision trace entries -> dicts (encoding: DESIGN.md §Parity)."""
     res = []
