@@ -129,6 +129,13 @@ int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, do
                      double* dV_phase, int32_t* trace);
 int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
 
+/* Running-cost gradient lx of knots 0..N-2 ([batch][N-1][n]) and terminal-cost gradient Phix
+ * ([batch][n]) of `phase` as the last partials evaluation left them: the reference's
+ * rcost_*[p][k].lx and tcost_*[p].Phix that print_debugInfo writes to cost.txt
+ * (MHPCLocomotion.cpp:355-377; AL terms in Phix only after forward_sweep(0), quirk B1).
+ * Either pointer may be NULL. */
+int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, double* Phix);
+
 /* The trial rollouts of MultiPhaseDDP::forward_iteration (MultiPhaseDDP.cpp:130-151, i.e.
  * SinglePhase::forward_sweep_dynamics_only, SinglePhase.cpp:117-144, chained over phases by
  * MultiPhaseDDP::forward_sweep_dynamics_only :56-76) at n_eps arbitrary step sizes, from the

@@ -146,21 +146,60 @@ class MHPCLocomotion {
     _tconstr_violation = viol[0];
   }
 
-  // state.txt / control.txt / gradient.txt of problem 0 (MHPCLocomotion.cpp:293-380)
+  // MHPCLocomotion::print_debugInfo (MHPCLocomotion.cpp:293-380) for one problem:
+  // state.txt, control.txt, gradient.txt, cost.txt in Eigen's default row format, with the
+  // reference's row counts -- including its N_TIMESTEPS[i+2] for the SRB phases of
+  // control / gradient / cost (exact for n_wbphase = 2; rows past an SRB phase's own N are
+  // the zero-initialised buffer; clamped where the reference would read past the array).
   void print_debugInfo(int problem = 0) {
-    std::ofstream fx("state.txt"), fu("control.txt"), fg("gradient.txt");
-    for (int p = 0; p < desc_.n_wb + desc_.n_fb; ++p) {
-      int n = 0, N = 0;
-      check(mhpc_phase_dims(&desc_, p, &n, &N), "mhpc_phase_dims");
-      std::vector<double> x((size_t)batch_ * N * n), u((size_t)batch_ * N * 4),
-          g((size_t)batch_ * N * n);
+    const int nwb = desc_.n_wb, nfb = desc_.n_fb, np = nwb + nfb;
+    struct Part { int n, N; std::vector<double> x, u, g, lx, phix; };
+    std::vector<Part> parts(np);
+    for (int p = 0; p < np; ++p) {
+      Part& q = parts[p];
+      check(mhpc_phase_dims(&desc_, p, &q.n, &q.N), "mhpc_phase_dims");
+      std::vector<double> x((size_t)batch_ * q.N * q.n), u((size_t)batch_ * q.N * 4),
+          g((size_t)batch_ * q.N * q.n), lx((size_t)batch_ * (q.N - 1) * q.n),
+          ph((size_t)batch_ * q.n);
       check(mhpc_get_phase(h_, p, x.data(), u.data(), nullptr, nullptr, nullptr, g.data()),
             "mhpc_get_phase");
-      for (int k = 0; k < N; ++k) {
-        write_row(fx, &x[((size_t)problem * N + k) * n], n);
-        write_row(fu, &u[((size_t)problem * N + k) * 4], 4);
-        write_row(fg, &g[((size_t)problem * N + k) * n], n);
-      }
+      check(mhpc_get_cost_gradients(h_, p, lx.data(), ph.data()), "mhpc_get_cost_gradients");
+      const size_t b = (size_t)problem;
+      q.x.assign(x.begin() + b * q.N * q.n, x.begin() + (b + 1) * q.N * q.n);
+      q.u.assign(u.begin() + b * q.N * 4, u.begin() + (b + 1) * q.N * 4);
+      q.g.assign(g.begin() + b * q.N * q.n, g.begin() + (b + 1) * q.N * q.n);
+      q.lx.assign(lx.begin() + b * (q.N - 1) * q.n, lx.begin() + (b + 1) * (q.N - 1) * q.n);
+      q.phix.assign(ph.begin() + b * q.n, ph.begin() + (b + 1) * q.n);
+    }
+    auto n_rows = [&](int i) { return i + 2 < np ? parts[i + 2].N : parts[nwb + i].N; };
+    // rows k < want of a [N][w] block, zero rows past N
+    auto block = [](std::ofstream& f, const std::vector<double>& a, int N, int w, int want) {
+      const std::vector<double> zero(w, 0.0);
+      for (int k = 0; k < want; ++k) write_row(f, k < N ? &a[(size_t)k * w] : zero.data(), w);
+    };
+    std::ofstream gradient_output("gradient.txt"), state_output("state.txt"),
+        contrl_output("control.txt"), cost_output("cost.txt");
+    std::printf("********** Write to file state.txt ************\n");
+    for (int i = 0; i < nwb; ++i) block(state_output, parts[i].x, parts[i].N, 14, parts[i].N);
+    for (int i = 0; i < nfb; ++i) {
+      const Part& q = parts[nwb + i];
+      block(state_output, q.x, q.N, 6, q.N);
+    }
+    std::printf("********** Write to file control.txt ************\n");
+    for (int i = 0; i < nwb; ++i) block(contrl_output, parts[i].u, parts[i].N, 4, parts[i].N);
+    for (int i = 0; i < nfb; ++i) block(contrl_output, parts[nwb + i].u, parts[nwb + i].N, 4, n_rows(i));
+    std::printf("********** Write to file gradient.txt ************\n");
+    for (int i = 0; i < nwb; ++i) block(gradient_output, parts[i].g, parts[i].N, 14, parts[i].N);
+    for (int i = 0; i < nfb; ++i) block(gradient_output, parts[nwb + i].g, parts[nwb + i].N, 6, n_rows(i));
+    std::printf("********** Write to file cost.txt ************\n");
+    for (int i = 0; i < nwb; ++i) {
+      block(cost_output, parts[i].lx, parts[i].N - 1, 14, parts[i].N - 1);
+      write_row(cost_output, parts[i].phix.data(), 14);
+    }
+    for (int i = 0; i < nfb; ++i) {
+      const Part& q = parts[nwb + i];
+      block(cost_output, q.lx, q.N - 1, 6, n_rows(i) - 1);
+      write_row(cost_output, q.phix.data(), 6);
     }
   }
 
@@ -174,13 +213,23 @@ class MHPCLocomotion {
     if (rc != MHPC_OK)
       throw std::runtime_error(std::string(what) + ": " + mhpc_last_error());
   }
+  // `ostream << vec.transpose()` with Eigen's default IOFormat: every coefficient printed
+  // like `ostream << double` (%g, 6 significant digits), right-aligned to the widest
+  // coefficient of the row, one space between coefficients
   static void write_row(std::ofstream& f, const double* v, int n) {
-    char buf[32];
+    std::vector<std::string> s(n);
+    size_t w = 0;
+    char buf[40];
     for (int i = 0; i < n; ++i) {
-      std::snprintf(buf, sizeof buf, "%g", v[i]);  // Eigen's default 6 significant digits
-      f << (i ? " " : "") << buf;
+      std::snprintf(buf, sizeof buf, "%g", v[i]);
+      s[i] = buf;
+      if (s[i].size() > w) w = s[i].size();
     }
-    f << "\n";
+    for (int i = 0; i < n; ++i) {
+      if (i) f << ' ';
+      f << std::string(w - s[i].size(), ' ') << s[i];
+    }
+    f << '\n';
   }
 
   int batch_;

@@ -114,6 +114,7 @@ SIGNATURES = [
     ("mhpc_get_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP]),
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
+    ("mhpc_get_cost_gradients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP]),
     ("mhpc_rollout_costs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP,
                                           ctypes.POINTER(ctypes.c_float)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),

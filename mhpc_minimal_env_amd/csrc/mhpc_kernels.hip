@@ -245,9 +245,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     st->cnt[C_LS_LAUNCH]++;
     if (conv) {
       st->ddp_active = 0;
+      st->ls_nt = nls < nc ? nls : nc;  // trials whose AL terms stay in Phix (see ProbState)
+      st->ls_nom = nom;
+      for (int p = 0; p < sp.P; ++p) { st->ls_sigma[p] = st->sigma[p]; st->ls_lambda[p] = st->lambda[p]; }
     } else {
       st->cnt[C_PAR]++;
       st->al_partials = 0;
+      st->par_slot = st->nom_slot;  // forward_sweep_partials_only (no AL terms, B1)
+      st->par_al = 0;
+      st->ls_nt = 0;
       if (ddp_iter < max_ddp) st->cnt[C_PAR_RUN]++;
       else st->ddp_active = 0;
     }
@@ -360,6 +366,76 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
 }
 
 // ============================================================================================
+// k_cost_grad: the running-cost gradient lx of every knot and the terminal-cost gradient
+// Phix of phase p as the last partials evaluation left them (rcost[k].lx, tcost.Phix;
+// CostBase.cpp:19-31,49-60 + the AL term of SinglePhase.cpp:257-275 when it was a
+// forward_sweep(0)), for print_debugInfo's cost.txt.  The constraint terms added to lx are
+// exact zeros (joint limits carry eps_ReB = 0; torque / GRF limits do not depend on x).
+// Lane = (problem, knot); lx [B][N-1][n], phix [B][n].
+// ============================================================================================
+__global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double* phix) {
+  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)sp.B * N) return;
+  const int b = (int)(t / N), k = (int)(t - (long)b * N);
+  const ProbState* st = &d.st[b];
+  const bool wb = p < sp.n_wb;
+  const int n = wb ? 14 : 6;
+  const double dt = sp.dt[p];
+  const double* x = traj_ptr(sp, d, b, st->par_slot, ko + k);
+  const double pos = d.refpos[(size_t)b * sp.NK + ko + k];
+  if (k < N - 1) {
+    double* o = lx + ((size_t)b * (N - 1) + k) * n;
+    for (int i = 0; i < n; ++i) {
+      double rxi, w2;
+      if (wb) {
+        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 2 ? 0.0
+              : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : 0.0;
+        w2 = 2 * dt * cQwb[i];
+      } else {
+        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
+        w2 = 2 * dt * cQfb[i];
+      }
+      o[i] = w2 * (x[i] - rxi);
+    }
+  } else {
+    double* o = phix + (size_t)b * n;
+    if (wb) {
+      double rx[14];
+      wb_term_ref(sp, mode, pos, rx);
+      const bool al = ntc_of(mode, true) && st->par_al;
+      double h = 0, hx[14], Hs[3][3];
+      if (al) {
+        if (mode == 2) wb_touchdown_compact<kFront>(x, &h, hx, Hs);
+        else wb_touchdown_compact<kBack>(x, &h, hx, Hs);
+      }
+      const double s = st->par_sigma[p], lam = st->par_lambda[p];
+      double v[14];
+      for (int i = 0; i < 14; ++i) {
+        v[i] = cQfwb[mode - 1][i] * (x[i] - rx[i]);
+        if (al) v[i] += 50 * (s * s / 2 * hx[i] * h + lam * hx[i]);
+      }
+      if (ntc_of(mode, true) && sp.AL_active) {  // trials of the last line search
+        const double s2 = st->ls_sigma[p], lam2 = st->ls_lambda[p];
+        for (int j = 0; j < st->ls_nt; ++j) {
+          const int slot = j < st->ls_nom ? j : j + 1;
+          const double* xt = traj_ptr(sp, d, b, slot, ko + k);
+          double ht, hxt[14], Hst[3][3];
+          if (mode == 2) wb_touchdown_compact<kFront>(xt, &ht, hxt, Hst);
+          else wb_touchdown_compact<kBack>(xt, &ht, hxt, Hst);
+          for (int i = 0; i < 14; ++i) v[i] += 50 * (s2 * s2 / 2 * hxt[i] * ht + lam2 * hxt[i]);
+        }
+      }
+      for (int i = 0; i < 14; ++i) o[i] = v[i];
+    } else {
+      double rx[6];
+      fb_term_ref(sp, pos, rx);
+      for (int i = 0; i < 6; ++i) o[i] = cQffb[i] * (x[i] - rx[i]);
+    }
+  }
+}
+
+// ============================================================================================
 // k_partials: one lane per (problem, knot, tangent direction)
 // ============================================================================================
 __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
@@ -467,6 +543,13 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d) {
   st->nom_slot = 0; st->al_iter = 0; st->ddp_iter = 0; st->bws_iter = 0; st->ntrace = 0;
   for (int i = 0; i < TRACE; ++i) st->trace[i] = -1;
   for (int i = 0; i < NCNT; ++i) st->cnt[i] = 0;
+  st->par_slot = 0;
+  st->par_al = 0;
+  st->ls_nt = 0;
+  st->ls_nom = 0;
+  for (int p = 0; p < MAXP; ++p) {
+    st->par_sigma[p] = 0; st->par_lambda[p] = 0; st->ls_sigma[p] = 0; st->ls_lambda[p] = 0;
+  }
   // warm start of the WB phases into slot 0 (bounding_PDcontrol, boundingPDControl.cpp:3-46)
   double x[14];
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
@@ -614,6 +697,10 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
     st->reb_active = reb ? 1 : 0;
     st->J = J;
     st->viol = sqrt(viol2);
+    st->par_slot = nom;  // forward_sweep(0) evaluated the partials (with AL, B1) here
+    st->par_al = sp.AL_active ? 1 : 0;
+    st->ls_nt = 0;
+    for (int p = 0; p < sp.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
     st->al_iter = al_iter;
     st->reg = 0;
     st->ddp_active = 1;
@@ -732,6 +819,13 @@ hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps
   const long n = (long)sp.B * n_eps;
   hipLaunchKernelGGL(k_eps_rollout, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, d, n_eps,
                      eps, J, viol);
+  return hipGetLastError();
+}
+hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, double* lx,
+                            double* phix, hipStream_t s) {
+  const long n = (long)sp.B * sp.N[p];
+  hipLaunchKernelGGL(k_cost_grad, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d, p, lx,
+                     phix);
   return hipGetLastError();
 }
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {

@@ -17,6 +17,7 @@ hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, hip
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
+hipError_t launch_cost_grad(const SolveParams&, const DevBufs&, int, double*, double*, hipStream_t);
 hipError_t launch_eps_rollout(const SolveParams&, const DevBufs&, int, const double*, double*,
                               double*, hipStream_t);
 hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
@@ -490,6 +491,27 @@ extern "C" int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, 
   cleanup();
   if (e != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("mhpc_rollout_costs: ") + hipGetErrorString(e));
   if (ms) *ms = t;
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, double* Phix) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+  const SolveParams& sp = h->sp;
+  if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
+  HIPCHK(hipSetDevice(h->device));
+  const int n = phase < sp.n_wb ? 14 : 6, N = sp.N[phase];
+  const size_t nlx = (size_t)sp.B * (N - 1) * n, nph = (size_t)sp.B * n;
+  double *dlx = nullptr, *dph = nullptr;
+  hipError_t e = hipMalloc((void**)&dlx, nlx * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dph, nph * sizeof(double));
+  if (e == hipSuccess) e = launch_cost_grad(sp, h->d, phase, dlx, dph, h->stream);
+  if (e == hipSuccess && lx) e = hipMemcpyAsync(lx, dlx, nlx * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && Phix) e = hipMemcpyAsync(Phix, dph, nph * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (dlx) (void)hipFree(dlx);
+  if (dph) (void)hipFree(dph);
+  if (e != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("mhpc_get_cost_gradients: ") + hipGetErrorString(e));
   return MHPC_OK;
 }
 

@@ -69,6 +69,17 @@ struct ProbState {
   int32_t ntrace;
   int32_t trace[TRACE];
   int64_t cnt[NCNT];
+  // state of the last running/terminal-cost partials evaluation (forward_sweep(0) or
+  // forward_sweep_partials_only) for print_debugInfo's cost.txt: the nominal slot it saw,
+  // whether the AL terms entered Phix (B1) and the sigma / lambda it used
+  int32_t par_slot, par_al;
+  double par_sigma[MAXP], par_lambda[MAXP];
+  // line-search trials run after that evaluation (only the final, converged line search of
+  // an AL iteration): the reference's dynamics-only sweeps add their AL terms to Phix too
+  // (guard quirk of SinglePhase.cpp:269), which cost.txt shows.  Trial j lives in slot
+  // j < ls_nom ? j : j + 1.
+  int32_t ls_nt, ls_nom;
+  double ls_sigma[MAXP], ls_lambda[MAXP];
 };
 
 struct DevBufs {

@@ -30,6 +30,15 @@ def f32(v: float) -> float:
     return float(np.float32(v))
 
 
+def eigen_row(v) -> str:
+    """One row as `ostream << vec.transpose()` prints it with Eigen's default IOFormat: each
+    coefficient formatted like `ostream << double` (6 significant digits, %g), right-aligned
+    to the widest coefficient of the row, separated by one space."""
+    strs = ["%g" % float(x) for x in np.ravel(v)]
+    w = max((len(t) for t in strs), default=0)
+    return " ".join(t.rjust(w) for t in strs)
+
+
 # ----------------------------------------------------------------------------------------
 @dataclass
 class HSDDP_OPTION:
@@ -316,17 +325,59 @@ class MHPCLocomotion:
             "G": np.concatenate([q["Vx"].reshape(B, -1) for q in parts], axis=1),
         }
 
-    def print_debugInfo(self, dirname: str = ".", problem: int = 0):
-        """state.txt / control.txt / gradient.txt of one problem (MHPCLocomotion.cpp:293-380,
-        without the reference's [i+2] indexing bug for n_wbphase != 2)."""
-        os.makedirs(dirname, exist_ok=True)
-        parts = [self.get_phase(p) for p in range(self.desc.n_phases)]
+    def get_cost_gradients(self, p: int) -> dict:
+        """lx [batch][N-1][n] and Phix [batch][n] of phase p as the last partials evaluation
+        left them (the reference's rcost[k].lx / tcost.Phix, written to cost.txt)."""
+        n = self.desc.xsize(p)
+        N = self.desc.N[p]
+        lx = np.zeros((self.batch, N - 1, n))
+        phix = np.zeros((self.batch, n))
+        capi.check(capi.lib().mhpc_get_cost_gradients(self._h, p, capi.dptr(lx), capi.dptr(phix)),
+                   "mhpc_get_cost_gradients")
+        return {"lx": lx, "Phix": phix}
 
-        def dump(fname, key):
+    def print_debugInfo(self, dirname: str = ".", problem: int = 0, verbose: bool = True):
+        """MHPCLocomotion::print_debugInfo (MHPCLocomotion.cpp:293-380) for one problem:
+        state.txt, control.txt, gradient.txt, cost.txt in Eigen's default row format
+        (eigen_row), with the reference's row counts -- including its N_TIMESTEPS[i+2]
+        indexing of the SRB phases in control / gradient / cost (exact for n_wbphase = 2;
+        rows past an SRB phase's own N are the zero-initialised buffer)."""
+        os.makedirs(dirname, exist_ok=True)
+        d = self.desc
+        nwb, nfb, P = d.n_wb, d.n_fb, d.n_phases
+        parts = [self.get_phase(p) for p in range(P)]
+        grads = [self.get_cost_gradients(p) for p in range(P)]
+        Ns = [d.N[p] for p in range(P)]
+
+        def n_rows(i):  # N_TIMESTEPS[i+2] (clamped where the reference would read past it)
+            return Ns[i + 2] if i + 2 < P else Ns[nwb + i]
+
+        def rows(arr, n_want, width):
+            out = [np.ravel(arr[k]) if k < len(arr) else np.zeros(width) for k in range(n_want)]
+            return out
+
+        def write(fname, blocks):
+            if verbose:
+                print(f"********** Write to file {fname} ************")
             with open(os.path.join(dirname, fname), "w") as f:
-                for q in parts:
-                    for row in q[key][problem]:
-                        f.write(" ".join(f"{v:.6g}" for v in np.ravel(row)) + "\n")
-        dump("state.txt", "x")
-        dump("control.txt", "u")
-        dump("gradient.txt", "Vx")
+                for blk in blocks:
+                    for r in blk:
+                        f.write(eigen_row(r) + "\n")
+
+        st, ct, gr, co = [], [], [], []
+        for i in range(nwb):
+            q, g = parts[i], grads[i]
+            st.append(rows(q["x"][problem], Ns[i], 14))
+            ct.append(rows(q["u"][problem], Ns[i], 4))
+            gr.append(rows(q["Vx"][problem], Ns[i], 14))
+            co.append(rows(g["lx"][problem], Ns[i] - 1, 14) + [g["Phix"][problem]])
+        for i in range(nfb):
+            q, g = parts[nwb + i], grads[nwb + i]
+            st.append(rows(q["x"][problem], Ns[nwb + i], 6))
+            ct.append(rows(q["u"][problem], n_rows(i), 4))
+            gr.append(rows(q["Vx"][problem], n_rows(i), 6))
+            co.append(rows(g["lx"][problem], n_rows(i) - 1, 6) + [g["Phix"][problem]])
+        write("state.txt", st)
+        write("control.txt", ct)
+        write("gradient.txt", gr)
+        write("cost.txt", co)

@@ -1163,3 +1163,40 @@ extern "C" int oracle_rollout_costs(const mhpc_problem_desc* desc, const mhpc_hs
   if (rollout_seconds) *rollout_seconds = ns.load() * 1e-9;  // summed over threads
   return 0;
 }
+
+// The cost gradients print_debugInfo writes to cost.txt (MHPCLocomotion.cpp:355-377) after
+// a solve: rcost[k].lx of knots 0..N-2 and tcost.Phix of every phase, phase-concatenated:
+// LX [batch][sum_p (N_p - 1) n_p], PHIX [batch][sum_p n_p].
+extern "C" int oracle_cost_gradients(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt,
+                                     int batch, const double* x0, int nthreads, double* LX,
+                                     double* PHIX) {
+  if (!g_ref.handle) return 3;
+  const int np = desc->n_wb + desc->n_fb;
+  if (np < 1 || np > MHPC_MAX_PHASES) return 1;
+  const int n0 = desc->n_wb > 0 ? 14 : 6;
+  std::atomic<int> next(0);
+  auto worker = [&]() {
+    for (;;) {
+      const int b = next.fetch_add(1);
+      if (b >= batch) break;
+      Problem P;
+      build(P, desc, opt, x0 + (size_t)b * n0);
+      mp_solve(P);
+      size_t llx = 0, lph = 0;
+      for (const Phase& ph : P.ph) { llx += (size_t)(ph.N - 1) * ph.n; lph += ph.n; }
+      double* lx = LX + (size_t)b * llx;
+      double* phx = PHIX + (size_t)b * lph;
+      for (const Phase& ph : P.ph) {
+        for (int k = 0; k < ph.N - 1; ++k)
+          for (int i = 0; i < ph.n; ++i) *lx++ = ph.rc[k].lx[i];
+        for (int i = 0; i < ph.n; ++i) *phx++ = ph.Phix[i];
+      }
+    }
+  };
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  return 0;
+}

@@ -105,6 +105,28 @@ def rollout_costs(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray,
     return {"J": J, "viol": viol, "rollout_cpu_seconds": secs.value}
 
 
+def cost_gradients(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray,
+                   nthreads: int = 1) -> dict:
+    """lx / Phix as print_debugInfo's cost.txt holds them after a solve; phase-concatenated
+    LX [batch][sum (N_p-1) n_p] and PHIX [batch][sum n_p]."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B = x0.shape[0]
+    llx = lph = 0
+    for p in range(desc.n_phases):
+        n = 14 if p < desc.n_wb else 6
+        llx += (desc.N[p] - 1) * n
+        lph += n
+    LX = np.zeros((B, llx))
+    PHIX = np.zeros((B, lph))
+    L = lib()
+    L.oracle_cost_gradients.restype = ctypes.c_int
+    rc = L.oracle_cost_gradients(ctypes.byref(desc), ctypes.byref(opt), ctypes.c_int(B), _p(x0),
+                                 ctypes.c_int(nthreads), _p(LX), _p(PHIX))
+    if rc != 0:
+        raise RuntimeError(f"oracle_cost_gradients failed ({rc})")
+    return {"LX": LX, "PHIX": PHIX}
+
+
 def decode_trace(t) -> list:
     """Decision trace entries -> dicts (encoding: DESIGN.md §Parity)."""
     res = []

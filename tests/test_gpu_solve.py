@@ -123,7 +123,8 @@ def test_reference_demo_cpp_driver(need_gpu, tmp_path):
     out = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True, check=True,
                          timeout=120).stdout
     J = float(re.search(r"J = (\S+)", out).group(1))
-    assert (tmp_path / "state.txt").exists() and (tmp_path / "gradient.txt").exists()
+    for f in ("state.txt", "control.txt", "gradient.txt", "cost.txt"):
+        assert (tmp_path / f).exists(), f
     lines = (tmp_path / "state.txt").read_text().strip().split("\n")
     assert len(lines) == 4 * 80 + 4 * 100
     O = _oracle()

@@ -70,3 +70,13 @@ def test_decode_trace():
     v = (2 << 24) | (1 << 23) | (1 << 22) | (11 << 8) | 3
     assert O.decode_trace([v, -1]) == [{"al": 2, "reb": 1, "conv": 1, "abort": 0, "n_ls": 11,
                                         "n_bws": 3}]
+
+
+def test_eigen_row_format():
+    """`ostream << VectorXd.transpose()` layout (Eigen default IOFormat): %g with 6
+    significant digits, right-aligned to the widest coefficient, single-space separated."""
+    from mhpc_minimal_env_amd.locomotion import eigen_row
+    assert eigen_row([0.5, -1.25, 100.0]) == "  0.5 -1.25   100"
+    assert eigen_row([1e-5, 0.0]) == "1e-05     0"
+    assert eigen_row([-0.0927, 1234567.0]) == "    -0.0927 1.23457e+06"
+    assert eigen_row([3.14159265]) == "3.14159"
