@@ -129,6 +129,25 @@ int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, do
                      double* dV_phase, int32_t* trace);
 int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c);
 
+/* Gait schedule (the reference's Gait class, Common/header/Gait.h:14-77): the mode cycle and
+ * the duration of every mode (timings[m-1], float as in the reference). */
+typedef struct {
+  int n_modes;
+  int modes[MHPC_MAX_PHASES];
+  float timings[MHPC_MAX_PHASES];
+} mhpc_gait;
+
+/* MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158), whole batch: advance the gait
+ * by one mode, rotate the WB / SRB phase buffers by one (the solution just computed becomes
+ * the warm start of the shifted horizon), recompute mode sequence and knot counts
+ * (round(timing / dt)), regenerate the references from the current x0 (set it first with
+ * mhpc_set_x0 -- the reference's set_initial_condition) and re-initialise the AL / ReB
+ * parameters.  Then call mhpc_solve again.  The phase descriptor reported by
+ * mhpc_get_desc changes accordingly. */
+int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait);
+/* The handle's current phase layout (changes with mhpc_update_problem). */
+int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc);
+
 /* Running-cost gradient lx of knots 0..N-2 ([batch][N-1][n]) and terminal-cost gradient Phix
  * ([batch][n]) of `phase` as the last partials evaluation left them: the reference's
  * rcost_*[p][k].lx and tcost_*[p].Phix that print_debugInfo writes to cost.txt

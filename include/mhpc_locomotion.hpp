@@ -78,6 +78,13 @@ class Gait {
     for (size_t i = 0; i < seq.size(); ++i) t[i] = timing_[seq[i] - 1];
     return t;
   }
+  mhpc_gait to_c() const {
+    mhpc_gait g{};
+    g.n_modes = (int)mode_.size();
+    for (size_t i = 0; i < mode_.size(); ++i) g.modes[i] = mode_[i];
+    for (size_t i = 0; i < timing_.size(); ++i) g.timings[i] = timing_[i];
+    return g;
+  }
 
  private:
   std::vector<int> mode_;
@@ -114,6 +121,7 @@ class MHPCLocomotion {
                              option.DDP_thresh, option.AL_thresh, option.AL_active,
                              option.ReB_active, option.smooth_active, 0};
     check(mhpc_create(&desc_, &opt_, batch_, device, &h_), "mhpc_create");
+    gait_ = gait->to_c();
     // default initial condition (MHPCLocomotion.cpp:37-39), projected if phase 0 is SRB
     const double x0[14] = {0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098,
                            0.9011, 0.2756,  0.7333,  0.0446, 0.0009,  1.3219, 2.7346};
@@ -129,6 +137,52 @@ class MHPCLocomotion {
 
   // extension: per-problem initial states [batch][xsize of phase 0]
   void set_initial_conditions(const std::vector<double>& x0) { x0_ = x0; }
+  // MultiPhaseDDP::set_initial_condition for every problem of the batch (same state)
+  void set_initial_condition(const std::vector<double>& x0) {
+    const int n0 = desc_.n_wb > 0 ? 14 : 6;
+    for (int b = 0; b < batch_; ++b)
+      for (int i = 0; i < n0; ++i) x0_[(size_t)b * n0 + i] = x0[i];
+  }
+
+  // MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158): gait advances one mode,
+  // phase buffers rotate (warm start), references follow the current initial condition
+  void update_problem() {
+    check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
+    check(mhpc_update_problem(h_, &gait_), "mhpc_update_problem");
+    check(mhpc_get_desc(h_, &desc_), "mhpc_get_desc");
+  }
+
+  // execution horizon of solve_mhpc (ms_exec / CTG_exec, MHPCLocomotion.cpp:176-194): nominal
+  // x [batch][Ne][14], u [batch][Ne][4], K [batch][Ne][4*14], du, G of phase 0 followed by
+  // phase 1 when there are two or more WB phases (Ne = N0 (+ N1))
+  struct ExecHorizon { int Ne = 0; std::vector<double> x, u, y, K, du, G; };
+  ExecHorizon get_exec() {
+    ExecHorizon e;
+    const int np = desc_.n_wb > 1 ? 2 : 1;
+    std::vector<int> Ns(np);
+    for (int p = 0; p < np; ++p) Ns[p] = desc_.N[p];
+    for (int p = 0; p < np; ++p) e.Ne += Ns[p];
+    const size_t B = batch_, Ne = e.Ne;
+    e.x.resize(B * Ne * 14); e.u.resize(B * Ne * 4); e.y.resize(B * Ne * 4);
+    e.K.resize(B * Ne * 56); e.du.resize(B * Ne * 4); e.G.resize(B * Ne * 14);
+    size_t off = 0;
+    for (int p = 0; p < np; ++p) {
+      const size_t N = Ns[p];
+      std::vector<double> x(B * N * 14), u(B * N * 4), y(B * N * 4), K(B * N * 56), du(B * N * 4),
+          G(B * N * 14);
+      check(mhpc_get_phase(h_, p, x.data(), u.data(), y.data(), K.data(), du.data(), G.data()),
+            "mhpc_get_phase");
+      for (size_t b = 0; b < B; ++b) {
+        auto cp = [&](std::vector<double>& dst, const std::vector<double>& src, size_t w) {
+          std::copy(src.begin() + b * N * w, src.begin() + (b + 1) * N * w,
+                    dst.begin() + (b * Ne + off) * w);
+        };
+        cp(e.x, x, 14); cp(e.u, u, 4); cp(e.y, y, 4); cp(e.K, K, 56); cp(e.du, du, 4); cp(e.G, G, 14);
+      }
+      off += N;
+    }
+    return e;
+  }
 
   void initialization() {  // (:47-53)
     check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
@@ -204,6 +258,7 @@ class MHPCLocomotion {
   }
 
   const std::vector<int32_t>& status() const { return status_; }
+  const mhpc_problem_desc& desc() const { return desc_; }
   mhpc_handle* handle() { return h_; }
 
   TH _actual_cost = 0, _exp_cost_change = 0, _tconstr_violation = 0;
@@ -233,6 +288,7 @@ class MHPCLocomotion {
   }
 
   int batch_;
+  mhpc_gait gait_{};
   mhpc_problem_desc desc_;
   mhpc_hsddp_option opt_;
   mhpc_handle* h_ = nullptr;

@@ -25,6 +25,15 @@ MHPC_SOLVE_REG_ABORT = 1
 MHPC_SOLVE_NONFINITE = 2
 
 
+class GaitC(ctypes.Structure):
+    """mhpc_gait: mode cycle + per-mode durations (the reference's Gait)."""
+    _fields_ = [
+        ("n_modes", ctypes.c_int32),
+        ("modes", ctypes.c_int32 * MHPC_MAX_PHASES),
+        ("timings", ctypes.c_float * MHPC_MAX_PHASES),
+    ]
+
+
 class ProblemDesc(ctypes.Structure):
     _fields_ = [
         ("n_wb", ctypes.c_int32),
@@ -115,6 +124,8 @@ SIGNATURES = [
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
     ("mhpc_get_cost_gradients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP]),
+    ("mhpc_update_problem", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GaitC)]),
+    ("mhpc_get_desc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ProblemDesc)]),
     ("mhpc_rollout_costs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP,
                                           ctypes.POINTER(ctypes.c_float)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),

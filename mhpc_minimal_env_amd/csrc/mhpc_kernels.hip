@@ -40,11 +40,14 @@ constexpr int RING_W = 22;  // doubles per ring record (x 14, u 4, y 4)
 
 // PIPE = false: the same wave plays both roles (no ring, registers hand over) -- better
 // once the batch fills the chip, when a second wave per block only competes for issue.
+// full = 1: forward_sweep(0) as a real rollout (one lane per problem, eps = 0, always
+// adopted) -- needed when the nominal is not a rollout of its own controls from x0, i.e.
+// after mhpc_update_problem (receding horizon); otherwise k_cost replaces it.
 template <bool PIPE>
 __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, DevBufs d,
                                                              int al_iter, int ddp_iter,
-                                                             int max_ddp) {
-  const int nc = sp.n_cand;
+                                                             int max_ddp, int full) {
+  const int nc = full ? 1 : sp.n_cand;
   const int ppw = 64 / nc;
   const int t = threadIdx.x, lane = t & 63;
   const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
@@ -63,15 +66,22 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   ProbState* st = nullptr;
   if (in) {
     st = &d.st[b];
-    run = st->active && st->ddp_active;
+    run = st->active && (full || st->ddp_active);
     nom = st->nom_slot;
     slot = j < nom ? j : j + 1;
   }
   if (w0 && run) sAny = 1;
   __syncthreads();
   if (!sAny) return;  // uniform: no problem of this block is still iterating
+  if (full && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
+    if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
+    const bool reb_off = (st->viol > 0.05) || al_iter == 1;
+    st->reb_active = (st->cap_reb && !reb_off) ? 1 : 0;
+    st->opt_reb = st->reb_active;
+  }
+  if (full) __syncthreads();
 
-  const double eps = run ? sp.eps[j] : 0.0;
+  const double eps = run && !full ? sp.eps[j] : 0.0;
   const bool reb = run && st->reb_active;
   double x[14];
   if (w0 && run) {
@@ -223,6 +233,25 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     sViol[lane] = sqrt(viol2);
   }
   __syncthreads();
+  if (full) {
+    if (w1 && run) {
+      st->J = J;
+      st->viol = sqrt(viol2);
+      for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][lane]; st->h[p] = sH[p][lane]; }
+      st->nom_slot = slot;
+      st->par_slot = slot;
+      st->par_al = sp.AL_active ? 1 : 0;
+      st->ls_nt = 0;
+      for (int p = 0; p < sp.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
+      st->al_iter = al_iter;
+      st->reg = 0;
+      st->ddp_active = 1;
+      st->al_partials = 1;
+      st->cnt[C_FWD]++;
+      st->cnt[C_PAR_RUN]++;
+    }
+    return;
+  }
   if (w1 && run && j == 0) {
     const double cost_prev = st->J;
     int sel = nc - 1, nls = nc + 1;
@@ -436,6 +465,64 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double
 }
 
 // ============================================================================================
+// Phase buffers of the receding-horizon loop (MHPCLocomotion::update_problem,
+// MHPCLocomotion.cpp:107-158): the reference keeps one N_TIMESTEPS_MAX-knot buffer per WB
+// and per SRB phase slot (nominal x,u,y and cost-to-go) and rotates which buffer each phase
+// uses.  store [B][P][nbk][SREC]: x,u,y (a traj record), K 56, du 4, G 14.  Phase p of the
+// current layout lives in buffer sp.buf[p].
+// ============================================================================================
+constexpr int SREC = KS + 56 + 4 + 14;
+
+__global__ void k_store_save(SolveParams sp, DevBufs d, double* store, int nbk) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)sp.B * sp.NK) return;
+  const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
+  int p = 0;
+  while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
+  const int k = kk - sp.ko[p];
+  double* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  const double* r = traj_ptr(sp, d, b, d.st[b].nom_slot, kk);
+  for (int i = 0; i < KS; ++i) o[i] = r[i];
+  const size_t rec = (size_t)b * sp.NK + kk;
+  for (int i = 0; i < 56; ++i) o[KS + i] = d.K[rec * 56 + i];
+  for (int i = 0; i < 4; ++i) o[KS + 56 + i] = d.du[rec * 4 + i];
+  for (int i = 0; i < 14; ++i) o[KS + 60 + i] = d.G[rec * 14 + i];
+}
+
+__global__ void k_store_load(SolveParams sp, DevBufs d, const double* store, int nbk) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)sp.B * sp.NK) return;
+  const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
+  int p = 0;
+  while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
+  const int k = kk - sp.ko[p];
+  const double* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  double* r = traj_ptr(sp, d, b, 0, kk);  // k_init(warm = 0) sets nom_slot = 0
+  for (int i = 0; i < KS; ++i) r[i] = o[i];
+  if (k == sp.N[p] - 1)  // u, y of the last knot are never rewritten by a sweep (B11): the
+    for (int sl = 1; sl < sp.nslot; ++sl) {  // buffer's stale tail must follow any trial
+      double* q = traj_ptr(sp, d, b, sl, kk);
+      for (int i = 0; i < KS; ++i) q[i] = o[i];
+    }
+  const size_t rec = (size_t)b * sp.NK + kk;
+  for (int i = 0; i < 56; ++i) d.K[rec * 56 + i] = o[KS + i];
+  for (int i = 0; i < 4; ++i) d.du[rec * 4 + i] = o[KS + 56 + i];
+  for (int i = 0; i < 14; ++i) d.G[rec * 14 + i] = o[KS + 60 + i];
+}
+
+hipError_t launch_store(const SolveParams& sp, const DevBufs& d, double* store, int nbk, int save,
+                        hipStream_t s) {
+  const long n = (long)sp.B * sp.NK;
+  if (save)
+    hipLaunchKernelGGL(k_store_save, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d,
+                       store, nbk);
+  else
+    hipLaunchKernelGGL(k_store_load, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d,
+                       store, nbk);
+  return hipGetLastError();
+}
+
+// ============================================================================================
 // k_partials: one lane per (problem, knot, tangent direction)
 // ============================================================================================
 __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
@@ -495,8 +582,9 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
   if (b >= sp.B) return;
   ProbState* st = &d.st[b];
   if (st->active) {
-    double up = sp.update_penalty;
+    double up = st->cap_pen;  // _option.update_penalty = captured value, 0 if satisfied
     if (st->viol < 0.03) up = 0;
+    st->opt_pen = up;
     for (int p = 0; p < sp.P; ++p) {
       const bool wb = p < sp.n_wb;
       if (ntc_of(sp.mode[p], wb)) st->lambda[p] += st->sigma[p] * st->h[p];
@@ -516,7 +604,10 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
 // ============================================================================================
 // initialization: references, state, PD warm start (MHPCLocomotion.cpp:47-53,200-215)
 // ============================================================================================
-__global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d) {
+// warm = 0 (mhpc_update_problem): references and per-problem state only -- the reference's
+// update_problem() regenerates the references and re-initialises the AL / ReB parameters of
+// every phase but keeps the (rotated) nominal trajectories and gains as the warm start.
+__global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= sp.B) return;
   const double* x0 = d.x0 + (size_t)b * 14;
@@ -550,6 +641,11 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d) {
   for (int p = 0; p < MAXP; ++p) {
     st->par_sigma[p] = 0; st->par_lambda[p] = 0; st->ls_sigma[p] = 0; st->ls_lambda[p] = 0;
   }
+  if (!warm) return;
+  st->opt_reb = sp.ReB_active ? 1 : 0;
+  st->opt_pen = sp.update_penalty;
+  st->cap_reb = st->opt_reb;
+  st->cap_pen = st->opt_pen;
   // warm start of the WB phases into slot 0 (bounding_PDcontrol, boundingPDControl.cpp:3-46)
   double x[14];
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
@@ -636,7 +732,9 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   __shared__ double sc[MHPC_MAX_KNOTS];
   __shared__ double sV[MAXP], sH[MAXP];
   const bool reb_off = (st->viol > 0.05) || al_iter == 1;
-  const bool reb = sp.ReB_active && !reb_off;
+  // solve() captures _option.ReB_active at its start, restores it every AL iteration
+  const int cap_reb = al_iter == 1 ? st->opt_reb : st->cap_reb;
+  const bool reb = cap_reb && !reb_off;
   const int nom = st->nom_slot;
   const double* refpos = d.refpos + (size_t)b * sp.NK;
   for (int kk = lane; kk < sp.NK; kk += 64) {
@@ -694,7 +792,9 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
       st->V[p] = sV[p];
       st->h[p] = sH[p];
     }
+    if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
     st->reb_active = reb ? 1 : 0;
+    st->opt_reb = st->reb_active;
     st->J = J;
     st->viol = sqrt(viol2);
     st->par_slot = nom;  // forward_sweep(0) evaluated the partials (with AL, B1) here
@@ -780,8 +880,12 @@ hipError_t launch_reduce_counters(const SolveParams& sp, const DevBufs& d,
   hipLaunchKernelGGL(k_reduce_counters, dim3((sp.B + 255) / 256), dim3(256), 0, s, sp, d, out);
   return hipGetLastError();
 }
+hipError_t launch_reset(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
+  hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
+  return hipGetLastError();
+}
 hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d);
+  hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, 1);
   return hipGetLastError();
 }
 hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hipStream_t s) {
@@ -790,7 +894,12 @@ hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hip
 }
 
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
-                          int max_ddp, hipStream_t s) {
+                          int max_ddp, int full, hipStream_t s) {
+  if (full) {
+    hipLaunchKernelGGL(k_rollout<false>, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, al_iter,
+                       0, 0, 1);
+    return hipGetLastError();
+  }
   const int ppw = 64 / sp.n_cand;
   const int nblk = (sp.B + ppw - 1) / ppw;
   static int ncu = 0;
@@ -808,10 +917,10 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
 #endif
   if (pipe)
     hipLaunchKernelGGL(k_rollout<true>, dim3(nblk), dim3(128), 0, s, sp, d, al_iter, ddp_iter,
-                       max_ddp);
+                       max_ddp, 0);
   else
     hipLaunchKernelGGL(k_rollout<false>, dim3(nblk), dim3(64), 0, s, sp, d, al_iter, ddp_iter,
-                       max_ddp);
+                       max_ddp, 0);
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/mhpc_capi.h"
@@ -13,10 +14,15 @@
 
 namespace mhpc {
 hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
-hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, hipStream_t);
+hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, double, hipStream_t);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
+hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_store(const SolveParams&, const DevBufs&, double*, int, int, hipStream_t);
+// N_TIMESTEPS_MAX (MHPCLocomotion.h): knots per phase buffer; record = x,u,y + K + du + G
+constexpr int kPhaseBufKnots = 110;
+constexpr int kStoreRec = KS + 56 + 4 + 14;
 hipError_t launch_cost_grad(const SolveParams&, const DevBufs&, int, double*, double*, hipStream_t);
 hipError_t launch_eps_rollout(const SolveParams&, const DevBufs&, int, const double*, double*,
                               double*, hipStream_t);
@@ -62,7 +68,7 @@ struct mhpc_handle {
   DevBufs d;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool x0_set = false, initialized = false, solved = false;
+  bool x0_set = false, initialized = false, solved = false, x0_changed = false;
   float solve_ms = 0;
   unsigned long long* dcnt = nullptr;  // reduced counters of the batch [NCNT]
   unsigned long long cnt[NCNT] = {};
@@ -74,7 +80,38 @@ struct mhpc_handle {
   int64_t klaunch[NKERN] = {};
   // algorithmic byte model per problem
   double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0, by_cost = 0;
+  // receding horizon (MHPCLocomotion::update_problem): current mode, phase-buffer rotation,
+  // buffer store, knot capacity of the packed arrays, and whether the next solve's first
+  // forward_sweep(0) must be a real rollout (rotated nominal, new x0)
+  int cmode = 1;
+  std::vector<int> pidx_wb, pidx_fb;
+  double* store = nullptr;
+  int nbk = 0, nk_cap = 0;
+  bool need_full = false;
+  bool store_valid = false;  // store zeroed since the last initialize (memory_reset)
 };
+
+// Phase layout of a descriptor: modes, knot counts and offsets, partials work items.
+static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
+  sp.P = desc.n_wb + desc.n_fb;
+  sp.n_wb = desc.n_wb;
+  int ko = 0, items = 0;
+  for (int p = 0; p < sp.P; ++p) {
+    const bool wb = p < desc.n_wb;
+    sp.mode[p] = desc.mode_seq[p];
+    sp.N[p] = desc.N[p];
+    sp.ko[p] = ko;
+    sp.xs[p] = wb ? 14 : 6;
+    sp.dt[p] = wb ? desc.dt_wb : desc.dt_fb;
+    ko += desc.N[p];
+    sp.par_item_off[p] = items;
+    if (wb) items += (desc.N[p] - 1) * 18 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
+  }
+  sp.par_item_off[sp.P] = items;
+  for (int p = sp.P + 1; p <= MAXP; ++p) sp.par_item_off[p] = items;
+  sp.par_items = items;
+  sp.NK = ko;
+}
 
 // Algorithmic HBM bytes (fp64) of one problem for each kernel's unit of work.
 static void byte_model(mhpc_handle* h) {
@@ -171,24 +208,8 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   SolveParams& sp = h->sp;
   memset(&sp, 0, sizeof sp);
   sp.B = batch;
-  sp.P = desc->n_wb + desc->n_fb;
-  sp.n_wb = desc->n_wb;
-  int ko = 0, items = 0;
-  for (int p = 0; p < sp.P; ++p) {
-    const bool wb = p < desc->n_wb;
-    sp.mode[p] = desc->mode_seq[p];
-    sp.N[p] = desc->N[p];
-    sp.ko[p] = ko;
-    sp.xs[p] = wb ? 14 : 6;
-    sp.dt[p] = wb ? desc->dt_wb : desc->dt_fb;
-    ko += desc->N[p];
-    sp.par_item_off[p] = items;
-    if (wb) items += (desc->N[p] - 1) * 18 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
-  }
-  sp.par_item_off[sp.P] = items;
-  for (int p = sp.P + 1; p <= MAXP; ++p) sp.par_item_off[p] = items;
-  sp.par_items = items;
-  sp.NK = ko;
+  layout_params(sp, *desc);
+  for (int p = 0; p < sp.P; ++p) sp.buf[p] = p;
   sp.vel = desc->vel_cmd;
   sp.height = desc->height_cmd;
   // line-search grid exactly as MultiPhaseDDP::forward_iteration generates it (:130-151)
@@ -231,6 +252,10 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   alloc((void**)&d.st, B * sizeof(ProbState));
   alloc((void**)&d.out, B * NK * KS * sizeof(double));
   alloc((void**)&h->dcnt, NCNT * sizeof(unsigned long long));
+  h->nk_cap = sp.NK;
+  h->nbk = kPhaseBufKnots;
+  for (int p = 0; p < sp.P; ++p) h->nbk = std::max(h->nbk, sp.N[p]);
+  alloc((void**)&h->store, B * sp.P * (size_t)h->nbk * kStoreRec * sizeof(double));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
@@ -241,6 +266,7 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   byte_model(h);
   if (e != hipSuccess) {
     if (h->dcnt) (void)hipFree(h->dcnt);
+    if (h->store) (void)hipFree(h->store);
     free_bufs(h);
     delete h;
     return fail(MHPC_ERR_DEVICE, std::string("allocation failed: ") + hipGetErrorString(e));
@@ -260,7 +286,7 @@ extern "C" int mhpc_set_x0(mhpc_handle* h, const double* x0) {
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->x0_set = true;
-  h->initialized = false;
+  h->x0_changed = true;  // references follow x0 only through initialize / update_problem
   return MHPC_OK;
 }
 
@@ -318,6 +344,16 @@ static int initialize_async(mhpc_handle* h) {
   HIPCHK(hipMemsetAsync(d.G, 0, B * NK * 14 * sizeof(double), h->stream));
   LAUNCH(h, K_INIT, launch_init(sp, d, h->stream));
   h->kbytes[K_INIT] += h->by_init * sp.B;
+  // build_problem binds phase p to buffer p; the buffer store is zeroed lazily (first
+  // update_problem), so a plain initialize + solve pays nothing for it
+  h->pidx_wb.clear();
+  h->pidx_fb.clear();
+  for (int i = 0; i < h->desc.n_wb; ++i) h->pidx_wb.push_back(i);
+  for (int i = 0; i < h->desc.n_fb; ++i) h->pidx_fb.push_back(i);
+  for (int p = 0; p < h->sp.P; ++p) h->sp.buf[p] = p;
+  h->cmode = h->desc.mode_seq[0];
+  h->store_valid = false;
+  h->need_full = false;
   return MHPC_OK;
 }
 
@@ -331,6 +367,7 @@ extern "C" int mhpc_initialize(mhpc_handle* h) {
   rc = collect_profile(h);
   if (rc) return rc;
   h->initialized = true;
+  h->x0_changed = false;
   h->solved = false;
   return MHPC_OK;
 }
@@ -344,13 +381,16 @@ static int solve_async(mhpc_handle* h) {
   int n_al = 0;
   for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
   for (int al = 1; al <= o.max_AL_iter; ++al) {
-    LAUNCH(h, K_FULL, launch_cost(sp, d, al, h->stream));  // forward_sweep(0)
+    if (al == 1 && h->need_full)  // rotated nominal from update_problem: a real rollout
+      LAUNCH(h, K_FULL, launch_rollout(sp, d, al, 0, 0, 1, h->stream));
+    else
+      LAUNCH(h, K_FULL, launch_cost(sp, d, al, h->stream));  // forward_sweep(0)
     LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     int max_ddp = 0;
     for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
     for (int ddp = 1; ddp <= max_ddp; ++ddp) {
       LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, h->stream));
-      LAUNCH(h, K_LS, launch_rollout(sp, d, al, ddp, max_ddp, h->stream));  // forward_iteration
+      LAUNCH(h, K_LS, launch_rollout(sp, d, al, ddp, max_ddp, 0, h->stream));  // forward_iteration
       if (ddp < max_ddp) LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
     }
     LAUNCH(h, K_AL, launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
@@ -365,7 +405,9 @@ static int solve_async(mhpc_handle* h) {
 extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
   if (!h->initialized) return fail(MHPC_ERR_STATE, "mhpc_initialize must precede mhpc_solve");
-  if (h->solved) return fail(MHPC_ERR_STATE, "solve already ran: call mhpc_initialize again");
+  if (h->solved) return fail(MHPC_ERR_STATE, "solve already ran: call mhpc_initialize or mhpc_update_problem");
+  if (h->x0_changed)
+    return fail(MHPC_ERR_STATE, "x0 changed: call mhpc_initialize or mhpc_update_problem first");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   int rc = solve_async(h);
@@ -376,6 +418,7 @@ extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) {
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipEventElapsedTime(&h->solve_ms, h->ev0, h->ev1));
   h->solved = true;
+  h->need_full = false;
   rc = collect_profile(h);
   if (rc) return rc;
   const unsigned long long* c = h->cnt;
@@ -515,6 +558,85 @@ extern "C" int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, do
   return MHPC_OK;
 }
 
+// MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158) for the whole batch: advance
+// the gait by one mode, rotate the WB and SRB phase buffers by one, recompute mode sequence
+// and knot counts, regenerate the references from the current x0 (mhpc_set_x0) and
+// re-initialise the AL / ReB parameters; the rotated nominal trajectories and gains are the
+// warm start of the next mhpc_solve, whose first forward_sweep(0) is then a real rollout.
+extern "C" int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait) {
+  if (!h || !gait) return fail(MHPC_ERR_INVALID, "null argument");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "mhpc_initialize must precede mhpc_update_problem");
+  if (gait->n_modes < 1 || gait->n_modes > MHPC_MAX_PHASES)
+    return fail(MHPC_ERR_INVALID, "gait needs 1..16 modes");
+  for (int i = 0; i < gait->n_modes; ++i)
+    if (gait->modes[i] < 1 || gait->modes[i] > 4) return fail(MHPC_ERR_INVALID, "gait mode out of range");
+  HIPCHK(hipSetDevice(h->device));
+  // Gait::get_next_mode / get_mode_seq / get_timings (Gait.h:48-77)
+  auto next_mode = [&](int m) {
+    for (int i = 0; i < gait->n_modes; ++i)
+      if (gait->modes[i] == m) return gait->modes[(i + 1) % gait->n_modes];
+    return -1;  // the reference falls off the end of a non-void function here
+  };
+  const int cm = next_mode(h->cmode);
+  if (cm < 0) return fail(MHPC_ERR_INVALID, "current mode is not in the gait");
+  mhpc_problem_desc nd = h->desc;
+  const int P = h->sp.P;
+  nd.mode_seq[0] = cm;
+  for (int p = 1; p < P; ++p) nd.mode_seq[p] = next_mode(nd.mode_seq[p - 1]);
+  for (int p = 0; p < P; ++p) {
+    const float tm = gait->timings[nd.mode_seq[p] - 1];
+    const double dt = p < nd.n_wb ? nd.dt_wb : nd.dt_fb;
+    nd.N[p] = (int)std::round((double)tm / dt);  // round(float timing / (double) dt)
+    if (nd.N[p] < 2) return fail(MHPC_ERR_INVALID, "gait timing gives a phase with N < 2");
+    if (nd.N[p] > h->nbk) return fail(MHPC_ERR_INVALID, "phase longer than the phase buffers");
+  }
+  if (!h->store_valid) {  // memory_reset of the buffers (lazy, see initialize_async)
+    HIPCHK(hipMemsetAsync(h->store, 0, (size_t)h->sp.B * P * h->nbk * kStoreRec * sizeof(double),
+                          h->stream));
+    h->store_valid = true;
+  }
+  // phases write through to their buffers in the reference: save the current layout
+  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, 1, h->stream));
+  // rotate the buffer lists (front -> back) and bind the new phases
+  if (!h->pidx_wb.empty()) std::rotate(h->pidx_wb.begin(), h->pidx_wb.begin() + 1, h->pidx_wb.end());
+  if (!h->pidx_fb.empty()) std::rotate(h->pidx_fb.begin(), h->pidx_fb.begin() + 1, h->pidx_fb.end());
+  SolveParams sp = h->sp;
+  layout_params(sp, nd);
+  for (int p = 0; p < P; ++p)
+    sp.buf[p] = p < nd.n_wb ? h->pidx_wb[p] : nd.n_wb + h->pidx_fb[p - nd.n_wb];
+  if (sp.NK > h->nk_cap) {  // grow the packed arrays (their content comes from the store)
+    HIPCHK(hipStreamSynchronize(h->stream));
+    DevBufs& d = h->d;
+    const size_t B = sp.B, NK = sp.NK;
+    double** arr[] = {&d.traj, &d.refpos, &d.K, &d.du, &d.G, &d.par, &d.out};
+    const size_t per[] = {(size_t)sp.nslot * KS, 1, 56, 4, 14, PS, KS};
+    for (int i = 0; i < 7; ++i) {
+      HIPCHK(hipFree(*arr[i]));
+      *arr[i] = nullptr;
+      HIPCHK(hipMalloc((void**)arr[i], B * NK * per[i] * sizeof(double)));
+    }
+    HIPCHK(hipMemsetAsync(d.traj, 0, B * sp.nslot * NK * KS * sizeof(double), h->stream));
+    h->nk_cap = sp.NK;
+  }
+  h->sp = sp;
+  h->desc = nd;
+  h->cmode = cm;
+  HIPCHK(launch_reset(h->sp, h->d, h->stream));  // refs from x0, AL/ReB init, nom_slot = 0
+  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, 0, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  byte_model(h);
+  h->need_full = true;
+  h->solved = false;
+  h->x0_changed = false;
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc) {
+  if (!h || !desc) return fail(MHPC_ERR_INVALID, "null argument");
+  *desc = h->desc;
+  return MHPC_OK;
+}
+
 extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) {
   if (!h || !c) return fail(MHPC_ERR_INVALID, "null argument");
   memset(c, 0, sizeof *c);
@@ -557,6 +679,7 @@ extern "C" void mhpc_destroy(mhpc_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_bufs(h);
   if (h->dcnt) (void)hipFree(h->dcnt);
+  if (h->store) (void)hipFree(h->store);
   for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);

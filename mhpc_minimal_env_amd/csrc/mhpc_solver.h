@@ -50,6 +50,7 @@ struct SolveParams {
       update_ReB;
   double eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
   int AL_active, ReB_active;
+  int buf[MAXP];             // phase buffer of each phase (receding horizon, see k_store_*)
   int par_items;             // partials work items per problem
   int par_item_off[MAXP + 1];  // prefix offsets of partials items per phase
 };
@@ -80,6 +81,12 @@ struct ProbState {
   // j < ls_nom ? j : j + 1.
   int32_t ls_nt, ls_nom;
   double ls_sigma[MAXP], ls_lambda[MAXP];
+  // MultiPhaseDDP::_option as solve() leaves it: ReB_active and update_penalty are rewritten
+  // inside the AL loop (MultiPhaseDDP.cpp:178-183, 273-277) and the next solve() starts from
+  // the rewritten values (captured at its first AL iteration: cap_*) -- visible across the
+  // solves of a receding-horizon loop.  mhpc_initialize restores the handle's options.
+  int32_t opt_reb, cap_reb;
+  double opt_pen, cap_pen;
 };
 
 struct DevBufs {

@@ -124,6 +124,15 @@ class Gait:
     def get_timings(self, mode_seq: List[int]) -> List[float]:
         return [self._gait_timing[m - 1] for m in mode_seq]
 
+    def to_c(self) -> capi.GaitC:
+        g = capi.GaitC()
+        g.n_modes = len(self._gait_mode)
+        for i, m in enumerate(self._gait_mode):
+            g.modes[i] = m
+        for i, t in enumerate(self._gait_timing):
+            g.timings[i] = t
+        return g
+
 
 def c_round(v: float) -> int:
     """C `round()` (half away from zero)."""
@@ -243,6 +252,25 @@ class MHPCLocomotion:
     def solve_mhpc(self) -> np.ndarray:
         capi.check(capi.lib().mhpc_solve(self._h, capi.iptr(self.status)), "mhpc_solve")
         return self.status
+
+    def update_problem(self, gait: Optional[Gait] = None):
+        """MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158) for every problem: the
+        gait advances one mode, the phase buffers rotate (warm start of the next solve), the
+        references follow the x0 given to set_initial_condition."""
+        L = capi.lib()
+        capi.check(L.mhpc_set_x0(self._h, capi.dptr(self._x0)), "mhpc_set_x0")
+        g = (gait or self.gait).to_c()
+        capi.check(L.mhpc_update_problem(self._h, __import__("ctypes").byref(g)),
+                   "mhpc_update_problem")
+        d = capi.ProblemDesc()
+        capi.check(L.mhpc_get_desc(self._h, __import__("ctypes").byref(d)), "mhpc_get_desc")
+        self.desc = d
+
+    def get_exec(self) -> dict:
+        """Execution horizon of solve_mhpc (MHPCLocomotion.cpp:176-194): the nominal and
+        cost-to-go of phase 0, followed by phase 1 when there are two WB phases."""
+        parts = [self.get_phase(0)] + ([self.get_phase(1)] if self.desc.n_wb > 1 else [])
+        return {k: np.concatenate([q[k] for q in parts], axis=1) for k in parts[0]}
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

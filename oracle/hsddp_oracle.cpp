@@ -1200,3 +1200,123 @@ extern "C" int oracle_cost_gradients(const mhpc_problem_desc* desc, const mhpc_h
   for (auto& t : th) t.join();
   return 0;
 }
+
+// Receding-horizon loop (f2): initialization() + solve, then per tick set_initial_condition,
+// MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158) and solve again.  Phase
+// buffers are emulated as the reference allocates them: one N_TIMESTEPS_MAX-knot buffer per
+// WB and per SRB phase slot holding the nominal (ModelState) and cost-to-go (CTG); phases
+// write through to their buffer, update_problem rotates which buffer each phase uses.
+// x0s [ticks][batch][n0]; per tick: J, viol [ticks][batch], trace [ticks][batch][TRACE],
+// N_out, modes_out [ticks][n_phases]; after the last tick the nominal X, U and K, G of every
+// phase, phase-concatenated into X [batch][cap_x] etc. with cap = n_phases * 110 knots.
+extern "C" int oracle_mpc(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt,
+                          int n_modes, const int* gait_modes, const float* gait_timings,
+                          int batch, int ticks, const double* x0s, int nthreads, double* J,
+                          double* viol, int32_t* trace, int32_t* N_out, int32_t* modes_out,
+                          double* X, double* U, double* K, double* G) {
+  if (!g_ref.handle) return 3;
+  const int np = desc->n_wb + desc->n_fb;
+  if (np < 1 || np > MHPC_MAX_PHASES || ticks < 1 || n_modes < 1) return 1;
+  const int n0 = desc->n_wb > 0 ? 14 : 6;
+  constexpr int NBK = 110;  // N_TIMESTEPS_MAX
+  std::atomic<int> next(0);
+  std::atomic<int> err(0);
+  auto next_mode = [&](int m) {
+    for (int i = 0; i < n_modes; ++i)
+      if (gait_modes[i] == m) return gait_modes[(i + 1) % n_modes];
+    return -1;
+  };
+  auto worker = [&]() {
+    for (;;) {
+      const int b = next.fetch_add(1);
+      if (b >= batch) break;
+      mhpc_problem_desc dl = *desc;
+      Problem P;
+      // ms_act_*, ms_nom_*, CTG_* buffers (the act buffer matters: its last knot's u, y are
+      // never written by a sweep and reach the nominal through update_nominal_trajectory)
+      struct Buf { std::vector<Knot> act, nom; std::vector<CTG> ctg; };
+      std::vector<Buf> bw(desc->n_wb), bf(desc->n_fb);
+      for (auto& q : bw) { q.act.assign(NBK, Knot{}); q.nom.assign(NBK, Knot{}); q.ctg.assign(NBK, CTG{}); }
+      for (auto& q : bf) { q.act.assign(NBK, Knot{}); q.nom.assign(NBK, Knot{}); q.ctg.assign(NBK, CTG{}); }
+      std::vector<int> pw(desc->n_wb), pf(desc->n_fb);
+      for (int i = 0; i < desc->n_wb; ++i) pw[i] = i;
+      for (int i = 0; i < desc->n_fb; ++i) pf[i] = i;
+      int cmode = dl.mode_seq[0];
+      for (int t = 0; t < ticks; ++t) {
+        const double* x0 = x0s + ((size_t)t * batch + b) * n0;
+        if (t == 0) {
+          build(P, &dl, opt, x0);
+        } else {
+          for (int p = 0; p < np; ++p) {  // phases wrote through to their buffers
+            Buf& q = p < dl.n_wb ? bw[pw[p]] : bf[pf[p - dl.n_wb]];
+            for (int k = 0; k < P.ph[p].N; ++k) {
+              q.act[k] = P.ph[p].act[k];
+              q.nom[k] = P.ph[p].nom[k];
+              q.ctg[k] = P.ph[p].ctg[k];
+            }
+          }
+          if (!pw.empty()) std::rotate(pw.begin(), pw.begin() + 1, pw.end());
+          if (!pf.empty()) std::rotate(pf.begin(), pf.begin() + 1, pf.end());
+          cmode = next_mode(cmode);
+          if (cmode < 0) { err = 4; return; }
+          dl.mode_seq[0] = cmode;
+          for (int p = 1; p < np; ++p) dl.mode_seq[p] = next_mode(dl.mode_seq[p - 1]);
+          for (int p = 0; p < np; ++p) {
+            const double dt = p < dl.n_wb ? dl.dt_wb : dl.dt_fb;
+            dl.N[p] = (int)round((double)gait_timings[dl.mode_seq[p] - 1] / dt);
+            if (dl.N[p] < 2 || dl.N[p] > NBK) { err = 5; return; }
+          }
+          for (int p = 0; p < np; ++p) {  // set_phase_config + set_data + initialization
+            Phase& ph = P.ph[p];
+            Buf& q = p < dl.n_wb ? bw[pw[p]] : bf[pf[p - dl.n_wb]];
+            ph.mode = dl.mode_seq[p];
+            ph.N = dl.N[p];
+            ph.act.assign(q.act.begin(), q.act.begin() + ph.N);
+            ph.nom.assign(q.nom.begin(), q.nom.begin() + ph.N);
+            ph.ref.assign(ph.N, Knot{});
+            ph.par.assign(ph.N, Par{});
+            ph.rc.assign(ph.N, RCost{});
+            ph.ctg.assign(q.ctg.begin(), q.ctg.begin() + ph.N);
+            init_params(ph);
+          }
+          memset(P.x0, 0, sizeof P.x0);
+          memcpy(P.x0, x0, sizeof(double) * P.ph[0].n);
+          generate_ref(P);
+          P.status = MHPC_SOLVE_OK;
+          P.ntrace = 0;
+          for (int i = 0; i < 6; ++i) P.cnt[i] = 0;
+        }
+        for (int i = 0; i < MHPC_TRACE_LEN; ++i) P.trace[i] = -1;
+        P.ntrace = 0;
+        mp_solve(P);
+        J[(size_t)t * batch + b] = P.actual_cost;
+        viol[(size_t)t * batch + b] = P.tconstr_violation;
+        memcpy(trace + ((size_t)t * batch + b) * MHPC_TRACE_LEN, P.trace,
+               sizeof(int32_t) * MHPC_TRACE_LEN);
+        if (b == 0)
+          for (int p = 0; p < np; ++p) {
+            N_out[t * np + p] = dl.N[p];
+            modes_out[t * np + p] = dl.mode_seq[p];
+          }
+      }
+      const size_t cap = (size_t)np * NBK;
+      double* xo = X + (size_t)b * cap * 14;
+      double* uo = U + (size_t)b * cap * 4;
+      double* ko = K + (size_t)b * cap * 56;
+      double* go = G + (size_t)b * cap * 14;
+      for (const Phase& ph : P.ph)
+        for (int k = 0; k < ph.N; ++k) {
+          for (int i = 0; i < ph.n; ++i) *xo++ = ph.nom[k].x[i];
+          for (int i = 0; i < 4; ++i) *uo++ = ph.nom[k].u[i];
+          for (int i = 0; i < 4 * ph.n; ++i) *ko++ = ph.ctg[k].K[i];
+          for (int i = 0; i < ph.n; ++i) *go++ = ph.ctg[k].G[i];
+        }
+    }
+  };
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  return err.load();
+}

@@ -127,6 +127,34 @@ def cost_gradients(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray
     return {"LX": LX, "PHIX": PHIX}
 
 
+def mpc(desc: capi.ProblemDesc, opt: capi.HsddpOption, gait, x0s: np.ndarray,
+        nthreads: int = 1) -> dict:
+    """Receding-horizon loop (oracle_mpc): initialization + solve, then per tick
+    set_initial_condition + update_problem + solve.  x0s [ticks][batch][n0]."""
+    x0s = np.ascontiguousarray(x0s, dtype=np.float64)
+    T, B = x0s.shape[0], x0s.shape[1]
+    P = desc.n_phases
+    cap = P * 110
+    g = gait.to_c()
+    modes = np.array(list(g.modes)[:g.n_modes], dtype=np.int32)
+    tim = np.array(list(g.timings)[:g.n_modes], dtype=np.float32)
+    out = {"J": np.zeros((T, B)), "viol": np.zeros((T, B)),
+           "trace": np.zeros((T, B, TRACE_LEN), dtype=np.int32),
+           "N": np.zeros((T, P), dtype=np.int32), "modes": np.zeros((T, P), dtype=np.int32),
+           "X": np.zeros((B, cap * 14)), "U": np.zeros((B, cap * 4)),
+           "K": np.zeros((B, cap * 56)), "G": np.zeros((B, cap * 14))}
+    L = lib()
+    L.oracle_mpc.restype = ctypes.c_int
+    rc = L.oracle_mpc(ctypes.byref(desc), ctypes.byref(opt), ctypes.c_int(int(g.n_modes)),
+                      _p(modes), _p(tim), ctypes.c_int(B), ctypes.c_int(T), _p(x0s),
+                      ctypes.c_int(nthreads), *[_p(out[k]) for k in
+                                                ("J", "viol", "trace", "N", "modes", "X", "U",
+                                                 "K", "G")])
+    if rc != 0:
+        raise RuntimeError(f"oracle_mpc failed ({rc})")
+    return out
+
+
 def decode_trace(t) -> list:
     """Decision trace entries -> dicts (encoding: DESIGN.md §Parity)."""
     res = []
