@@ -525,34 +525,61 @@ hipError_t launch_store(const SolveParams& sp, const DevBufs& d, double* store, 
 // ============================================================================================
 // k_partials: one lane per (problem, knot, tangent direction)
 // ============================================================================================
-__global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
+// Two launches with their own register allocation: VC = false takes the configuration
+// directions (full dual arithmetic, 7 per knot) and the impact Jacobian, VC = true the
+// velocity / control directions (11 per knot), where M, its factorisation and the
+// Jacobians stay plain doubles -- their derivative is exactly zero there.
+#ifndef MHPC_PAR_WAVES
+#define MHPC_PAR_WAVES 1
+#endif
+#ifndef MHPC_PARV_WAVES
+#define MHPC_PARV_WAVES 1
+#endif
+template <bool VC>
+__global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_partials(
+    SolveParams sp, DevBufs d) {
+  const int items = VC ? sp.par_items_v : sp.par_items;
+  const int* off = VC ? sp.par_v_off : sp.par_item_off;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = (int)(t / sp.par_items);
+  const int b = (int)(t / items);
   if (b >= sp.B) return;
-  const int it = (int)(t - (long)b * sp.par_items);
+  const int it = (int)(t - (long)b * items);
   const ProbState* st = &d.st[b];
   if (!(st->active && st->ddp_active)) return;
   int p = 0;
-  while (it >= sp.par_item_off[p + 1]) ++p;
-  const int loc = it - sp.par_item_off[p];
+  while (it >= off[p + 1]) ++p;
+  const int loc = it - off[p];
   const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
   const int nom = st->nom_slot;
-  if (loc < (N - 1) * 18) {
-    const int k = loc / 18, dir = loc - k * 18;
+  if (VC || loc < (N - 1) * 7) {
+    const int k = VC ? loc / 11 : loc / 7;
+    const int dir = VC ? 7 + (loc - k * 11) : loc - k * 7;
     const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-    Dual x[14], u[4], f[14], y[4];
-#pragma unroll
-    for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? 1.0 : 0.0);
+    Dual u[4], f[14], y[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = Dual(nk[14 + i], 14 + i == dir ? 1.0 : 0.0);
-    wb_dynamics<Dual>(x, u, mode, f, y);
+    if (!VC) {
+      Dual x[14];
+#pragma unroll
+      for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? 1.0 : 0.0);
+      wb_dynamics<Dual>(x, u, mode, f, y);
+    } else {
+      double xq[7];
+      Dual xv[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        xq[i] = nk[i];
+        xv[i] = Dual(nk[7 + i], 7 + i == dir ? 1.0 : 0.0);
+      }
+      wb_dynamics_qv<double, Dual>(xq, xv, u, mode, f, y);
+    }
     double* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
     double* out = rec + dir * 9;
 #pragma unroll
     for (int i = 0; i < 7; ++i) out[i] = f[7 + i].d;
     out[7] = mode == 1 ? y[2].d : y[0].d;
     out[8] = mode == 1 ? y[3].d : y[1].d;
-    if (dir == 0) {
+    if (!VC && dir == 0) {
       // running-cost derivatives of controls and contact forces at the nominal knot
       // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
       double c[14];
@@ -562,7 +589,7 @@ __global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
       for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
     }
   } else {
-    const int dir = loc - (N - 1) * 18;
+    const int dir = loc - (N - 1) * 7;
     const double* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
     Dual x[14], xp[14], lam[2];
 #pragma unroll
@@ -938,9 +965,11 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, doub
   return hipGetLastError();
 }
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  const long total = (long)sp.B * sp.par_items;
-  if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_partials, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sp, d);
+  const long tq = (long)sp.B * sp.par_items, tv = (long)sp.B * sp.par_items_v;
+  if (tq > 0)
+    hipLaunchKernelGGL(k_partials<false>, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s, sp, d);
+  if (tv > 0)
+    hipLaunchKernelGGL(k_partials<true>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, sp, d);
   return hipGetLastError();
 }
 hipError_t launch_al_end(const SolveParams& sp, const DevBufs& d, int last, hipStream_t s) {

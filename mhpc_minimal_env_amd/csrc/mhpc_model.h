@@ -54,30 +54,39 @@ constexpr int kFbX = 6, kFbU = 4, kFbY = 4;
 
 enum Foot { kFront = 0, kBack = 1 };
 
+// Two scalar types run through the model: Q for everything that depends on the
+// configuration q only (link sines/cosines, Jacobians, M and its factorisation) and V for
+// what also depends on qdot or u (link rates, bias h, Jdot qdot, accelerations, forces).
+// Q = V = double is the plain model; Q = V = Dual differentiates along a q direction; Q =
+// double, V = Dual differentiates along a qdot or u direction, where M, its factorisation
+// and the Jacobians carry exactly zero derivative -- the same numbers at a fraction of the
+// work (the Jacobian pass, k_partials).
+
 // Geometry of one leg: absolute link angles and their sines/cosines.
-template <class S>
+template <class Q, class V>
 struct LegGeo {
-  S s1, c1, s2, c2;  // thigh angle a1 = th + q_hip, shank angle a2 = a1 + q_knee
-  S w1, w2;          // absolute angular rates
+  Q s1, c1, s2, c2;  // thigh angle a1 = th + q_hip, shank angle a2 = a1 + q_knee
+  V w1, w2;          // absolute angular rates
 };
 
-template <class S>
+template <class Q, class V>
 struct WbGeo {
-  S sth, cth;        // body pitch
-  LegGeo<S> leg[2];  // [front, back]
+  Q sth, cth;           // body pitch
+  LegGeo<Q, V> leg[2];  // [front, back]
 };
 
-template <class S>
-MHPC_HD void wb_geometry(const S* x, WbGeo<S>& g) {
-  sin_cos(x[2], &g.sth, &g.cth);
+// xq = q (7), xv = qdot (7)
+template <class Q, class V>
+MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g) {
+  sin_cos(xq[2], &g.sth, &g.cth);
   for (int f = 0; f < 2; ++f) {
     const int ih = 3 + 2 * f, ik = 4 + 2 * f;
-    const S a1 = x[2] + x[ih];
-    const S a2 = a1 + x[ik];
+    const Q a1 = xq[2] + xq[ih];
+    const Q a2 = a1 + xq[ik];
     sin_cos(a1, &g.leg[f].s1, &g.leg[f].c1);
     sin_cos(a2, &g.leg[f].s2, &g.leg[f].c2);
-    g.leg[f].w1 = x[9] + x[7 + ih];
-    g.leg[f].w2 = g.leg[f].w1 + x[7 + ik];
+    g.leg[f].w1 = xv[2] + xv[ih];
+    g.leg[f].w2 = g.leg[f].w1 + xv[ik];
   }
 }
 
@@ -86,16 +95,16 @@ MHPC_HD void wb_geometry(const S* x, WbGeo<S>& g) {
 // Jdot*qdot due to the two link rotations (the hip-offset part is added by the caller).
 // The leg index is a template parameter everywhere so that no register array is indexed
 // with a run-time value (which would spill it to scratch memory on the GPU).
-template <class S, int F>
-MHPC_HD void leg_point_jac(const WbGeo<S>& g, double l1, double l2, S jx[5], S jz[5], S* jdx,
-                           S* jdz) {
+template <class Q, class V, int F>
+MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, double l1, double l2, Q jx[5], Q jz[5], V* jdx,
+                           V* jdz) {
   constexpr double sg = F == kFront ? 1.0 : -1.0;
-  const LegGeo<S>& L = g.leg[F];
+  const LegGeo<Q, V>& L = g.leg[F];
   // d/da of l*(-sin a, -cos a) = l*(-cos a, sin a)
-  const S tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
-  const S tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
-  jx[0] = S(1.0); jz[0] = S(0.0);
-  jx[1] = S(0.0); jz[1] = S(1.0);
+  const Q tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
+  const Q tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
+  jx[0] = Q(1.0); jz[0] = Q(0.0);
+  jx[1] = Q(0.0); jz[1] = Q(1.0);
   jx[4] = tx2;    jz[4] = tz2;
   jx[3] = tx1 + tx2;
   jz[3] = tz1 + tz2;
@@ -108,29 +117,30 @@ MHPC_HD void leg_point_jac(const WbGeo<S>& g, double l1, double l2, S jx[5], S j
 // Packed lower-triangular index of the symmetric 7x7 mass matrix.
 MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
-// Contribution of the thigh and shank of leg F to M (packed) and h.
-template <class S, int F>
-MHPC_HD void add_leg(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
+// Contribution of the thigh and shank of leg F to M (packed) and h.  xv = qdot.
+template <class Q, class V, int F>
+MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
   constexpr double sg = F == kFront ? 1.0 : -1.0;
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
-  const S thd2 = x[9] * x[9];
-  const S hax = (-sg * kHipX) * g.cth * thd2;  // centripetal acceleration of the hip point
-  const S haz = (sg * kHipX) * g.sth * thd2;
+  const V thd2 = xv[2] * xv[2];
+  const V hax = (-sg * kHipX) * g.cth * thd2;  // centripetal acceleration of the hip point
+  const V haz = (sg * kHipX) * g.sth * thd2;
 #pragma unroll
   for (int b = 0; b < 2; ++b) {  // thigh, shank
-    S jx[5], jz[5], jdx, jdz;
+    Q jx[5], jz[5];
+    V jdx, jdz;
     double m, ic;
     if (b == 0) {
-      leg_point_jac<S, F>(g, kThighCom, 0.0, jx, jz, &jdx, &jdz);
+      leg_point_jac<Q, V, F>(g, kThighCom, 0.0, jx, jz, &jdx, &jdz);
       m = kThighMass; ic = kThighInertiaCom;
     } else {
-      leg_point_jac<S, F>(g, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
+      leg_point_jac<Q, V, F>(g, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
       m = kShankMass; ic = kShankInertiaCom;
     }
     const int nc = b == 0 ? 4 : 5;
     jdx += hax;
     jdz += haz;
-    const S ax = jdx, az = jdz + kGrav;
+    const V ax = jdx, az = jdz + kGrav;
 #pragma unroll
     for (int a = 0; a < 5; ++a) {
       if (a >= nc) continue;
@@ -139,10 +149,10 @@ MHPC_HD void add_leg(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
       for (int c = 0; c <= a; ++c) {
         // x/z columns of a CoM Jacobian are unit vectors: skip the exact zeros
         if (a < 2 && c < 2) {
-          if (a == c) M[tri(idx[a], idx[c])] += S(m);
+          if (a == c) M[tri(idx[a], idx[c])] += Q(m);
           continue;
         }
-        S v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
+        Q v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
         if (a >= 2 && c >= 2) v += ic;
         M[tri(idx[a], idx[c])] += v;
       }
@@ -151,18 +161,18 @@ MHPC_HD void add_leg(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
 }
 
 // M(q) (packed lower triangle, 28 entries) and bias h(q, qdot) = C qdot + g.
-template <class S>
-MHPC_HD void wb_mass_bias(const S* x, const WbGeo<S>& g, S M[28], S h[7]) {
+template <class Q, class V>
+MHPC_HD void wb_mass_bias(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
 #pragma unroll
-  for (int i = 0; i < 7; ++i) h[i] = S(0.0);
+  for (int i = 0; i < 7; ++i) h[i] = V(0.0);
 #pragma unroll
-  for (int i = 0; i < 28; ++i) M[i] = S(0.0);
-  M[tri(0, 0)] = S(kBodyMass);
-  M[tri(1, 1)] = S(kBodyMass);
-  M[tri(2, 2)] = S(kBodyInertia);
-  h[1] = S(kBodyMass * kGrav);
-  add_leg<S, kFront>(x, g, M, h);
-  add_leg<S, kBack>(x, g, M, h);
+  for (int i = 0; i < 28; ++i) M[i] = Q(0.0);
+  M[tri(0, 0)] = Q(kBodyMass);
+  M[tri(1, 1)] = Q(kBodyMass);
+  M[tri(2, 2)] = Q(kBodyInertia);
+  h[1] = V(kBodyMass * kGrav);
+  add_leg<Q, V, kFront>(xv, g, M, h);
+  add_leg<Q, V, kBack>(xv, g, M, h);
 }
 
 // Block-arrowhead factorisation of the mass matrix.  Ordered (base x,z,th | front leg |
@@ -218,11 +228,11 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   F.Si[5] = (s00 * s11 - s10 * s10) * rdet;
 }
 
-// b <- M^-1 b
-template <class S>
-MHPC_HD void arrow_solve(const S M[28], const ArrowFactor<S>& F, S b[7]) {
-  S w[2][2];
-  S r0 = b[0], r1 = b[1], r2 = b[2];
+// b <- M^-1 b  (M, factor in Q; b in V)
+template <class Q, class V>
+MHPC_HD void arrow_solve(const Q M[28], const ArrowFactor<Q>& F, V b[7]) {
+  V w[2][2];
+  V r0 = b[0], r1 = b[1], r2 = b[2];
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
@@ -232,9 +242,9 @@ MHPC_HD void arrow_solve(const S M[28], const ArrowFactor<S>& F, S b[7]) {
     r1 -= M[tri(i0, 1)] * w[l][0] + M[tri(i1, 1)] * w[l][1];
     r2 -= M[tri(i0, 2)] * w[l][0] + M[tri(i1, 2)] * w[l][1];
   }
-  const S x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
-  const S x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
-  const S x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
+  const V x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
+  const V x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
+  const V x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
   b[0] = x0;
   b[1] = x1;
   b[2] = x2;
@@ -245,18 +255,19 @@ MHPC_HD void arrow_solve(const S M[28], const ArrowFactor<S>& F, S b[7]) {
   }
 }
 
-// Foot Jacobian (2x7, dense) and Jdot*qdot of foot F.
-template <class S, int F>
-MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, S J[2][7], S jd[2]) {
-  S jx[5], jz[5], jdx, jdz;
-  leg_point_jac<S, F>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
+// Foot Jacobian (2x7, dense) and Jdot*qdot of foot F.  xv = qdot.
+template <class Q, class V, int F>
+MHPC_HD void wb_foot_jac_full(const V* xv, const WbGeo<Q, V>& g, Q J[2][7], V jd[2]) {
+  Q jx[5], jz[5];
+  V jdx, jdz;
+  leg_point_jac<Q, V, F>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
   constexpr double sg = F == kFront ? 1.0 : -1.0;
-  const S thd2 = x[9] * x[9];
+  const V thd2 = xv[2] * xv[2];
   jd[0] = jdx + (-sg * kHipX) * g.cth * thd2;
   jd[1] = jdz + (sg * kHipX) * g.sth * thd2;
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
 #pragma unroll
-  for (int i = 0; i < 7; ++i) { J[0][i] = S(0.0); J[1][i] = S(0.0); }
+  for (int i = 0; i < 7; ++i) { J[0][i] = Q(0.0); J[1][i] = Q(0.0); }
 #pragma unroll
   for (int a = 0; a < 5; ++a) { J[0][idx[a]] = jx[a]; J[1][idx[a]] = jz[a]; }
 }
@@ -264,17 +275,18 @@ MHPC_HD void wb_foot_jac_full(const S* x, const WbGeo<S>& g, S J[2][7], S jd[2])
 // Schur-complement solve of the contact KKT system
 //   [M -J'; J 0] [v; lam] = [rhs; -c]  ->  v = M^-1 (rhs + J' lam)
 // given the factorisation of M; v holds M^-1 rhs on entry.
-template <class S>
-MHPC_HD void kkt_contact(const S M[28], const ArrowFactor<S>& F, const S J[2][7], const S c[2],
-                         S v[7], S lam[2]) {
-  S Y[2][7];
+template <class Q, class V>
+MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7], const V c[2],
+                         V v[7], V lam[2]) {
+  Q Y[2][7];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) Y[r][i] = J[r][i];
-    arrow_solve(M, F, Y[r]);
+    arrow_solve<Q, Q>(M, F, Y[r]);
   }
-  S A00 = S(0.0), A01 = S(0.0), A11 = S(0.0), r0 = -c[0], r1 = -c[1];
+  Q A00 = Q(0.0), A01 = Q(0.0), A11 = Q(0.0);
+  V r0 = -c[0], r1 = -c[1];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     A00 += J[0][i] * Y[0][i];
@@ -283,7 +295,7 @@ MHPC_HD void kkt_contact(const S M[28], const ArrowFactor<S>& F, const S J[2][7]
     r0 -= J[0][i] * v[i];
     r1 -= J[1][i] * v[i];
   }
-  const S rdet = S(1.0) / (A00 * A11 - A01 * A01);
+  const Q rdet = Q(1.0) / (A00 * A11 - A01 * A01);
   lam[0] = (A11 * r0 - A01 * r1) * rdet;
   lam[1] = (A00 * r1 - A01 * r0) * rdet;
 #pragma unroll
@@ -291,61 +303,70 @@ MHPC_HD void kkt_contact(const S M[28], const ArrowFactor<S>& F, const S J[2][7]
 }
 
 // Stance dynamics with foot F on the ground (Dyn_FS: F = front, Dyn_BS: F = back).
-template <class S, int F>
-MHPC_HD void wb_stance(const S* x, const WbGeo<S>& g, const S M[28], const ArrowFactor<S>& AF,
-                       S v[7], S* y) {
-  S J[2][7], jd[2], lam[2];
-  wb_foot_jac_full<S, F>(x, g, J, jd);
-  kkt_contact(M, AF, J, jd, v, lam);
+template <class Q, class V, int F>
+MHPC_HD void wb_stance(const V* xv, const WbGeo<Q, V>& g, const Q M[28],
+                       const ArrowFactor<Q>& AF, V v[7], V* y) {
+  Q J[2][7];
+  V jd[2], lam[2];
+  wb_foot_jac_full<Q, V, F>(xv, g, J, jd);
+  kkt_contact<Q, V>(M, AF, J, jd, v, lam);
   y[2 * F] = lam[0];
   y[2 * F + 1] = lam[1];
 }
 
-// Continuous whole-body dynamics: xdot = (qdot, qddot), y = contact force of the stance
-// foot in its slots (front -> y[0:2], back -> y[2:4]); zero in flight.
-// mode 1: back stance (Dyn_BS), 2/4: flight (Dyn_FL), 3: front stance (Dyn_FS).
-template <class S>
-MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
-  WbGeo<S> g;
-  wb_geometry(x, g);
-  S M[28], h[7];
-  wb_mass_bias(x, g, M, h);
-  ArrowFactor<S> AF;
+// Continuous whole-body dynamics with q in Q and (qdot, u) in V: xdot = (qdot, qddot),
+// y = contact force of the stance foot in its slots (front -> y[0:2], back -> y[2:4]);
+// zero in flight.  mode 1: back stance (Dyn_BS), 2/4: flight (Dyn_FL), 3: front stance
+// (Dyn_FS).
+template <class Q, class V>
+MHPC_HD void wb_dynamics_qv(const Q* xq, const V* xv, const V* u, int mode, V* xdot, V* y) {
+  WbGeo<Q, V> g;
+  wb_geometry<Q, V>(xq, xv, g);
+  Q M[28];
+  V h[7];
+  wb_mass_bias<Q, V>(xv, g, M, h);
+  ArrowFactor<Q> AF;
   arrow_factor(M, AF);
-  S v[7];
+  V v[7];
   v[0] = -h[0]; v[1] = -h[1]; v[2] = -h[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
-  arrow_solve(M, AF, v);
+  arrow_solve<Q, V>(M, AF, v);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = S(0.0);
-  if (mode == 1) wb_stance<S, kBack>(x, g, M, AF, v, y);
-  else if (mode == 3) wb_stance<S, kFront>(x, g, M, AF, v, y);
+  for (int i = 0; i < 4; ++i) y[i] = V(0.0);
+  if (mode == 1) wb_stance<Q, V, kBack>(xv, g, M, AF, v, y);
+  else if (mode == 3) wb_stance<Q, V, kFront>(xv, g, M, AF, v, y);
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
-    xdot[i] = x[7 + i];
+    xdot[i] = xv[i];
     xdot[7 + i] = v[i];
   }
+}
+
+// The plain interface: x = (q, qdot) in one scalar type.
+template <class S>
+MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
+  wb_dynamics_qv<S, S>(x, x + 7, u, mode, xdot, y);
 }
 
 // Plastic impact of foot F (Imp_F: front, end of mode 2; Imp_B: back, end of mode 4):
 // q+ = q, [M -J'; J 0][qd+; Lam] = [M qd-; 0].
 template <class S, int F>
 MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
-  WbGeo<S> g;
-  wb_geometry(x, g);
+  WbGeo<S, S> g;
+  wb_geometry<S, S>(x, x + 7, g);
   S M[28], h[7];
-  wb_mass_bias(x, g, M, h);
+  wb_mass_bias<S, S>(x + 7, g, M, h);
   ArrowFactor<S> AF;
   arrow_factor(M, AF);
   S J[2][7], jd[2];
-  wb_foot_jac_full<S, F>(x, g, J, jd);
+  wb_foot_jac_full<S, S, F>(x + 7, g, J, jd);
   S v[7], c[2];
 #pragma unroll
   for (int i = 0; i < 7; ++i) v[i] = x[7 + i];  // M^-1 (M qd-) = qd-
   c[0] = S(0.0);
   c[1] = S(0.0);
-  kkt_contact(M, AF, J, c, v, Lam);  // J qd+ = 0
+  kkt_contact<S, S>(M, AF, J, c, v, Lam);  // J qd+ = 0
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     xp[i] = x[i];
@@ -413,16 +434,16 @@ MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double*
 // (Jacob_F / Jacob_B; boundingPDControl.cpp:29,35).
 template <int F>
 MHPC_HD void wb_foot_jacobian_f(const double* x, double* J, double* Jd) {
-  WbGeo<double> g;
-  wb_geometry(x, g);
+  WbGeo<double, double> g;
+  wb_geometry<double, double>(x, x + 7, g);
   double Jm[2][7], jd[2];
-  wb_foot_jac_full<double, F>(x, g, Jm, jd);
+  wb_foot_jac_full<double, double, F>(x + 7, g, Jm, jd);
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
     for (int i = 0; i < 7; ++i) J[r * 7 + i] = Jm[r][i];
   constexpr double sg = F == kFront ? 1.0 : -1.0;
-  const LegGeo<double>& L = g.leg[F];
+  const LegGeo<double, double>& L = g.leg[F];
   const double thd = x[9];
 #pragma unroll
   for (int i = 0; i < 14; ++i) Jd[i] = 0.0;

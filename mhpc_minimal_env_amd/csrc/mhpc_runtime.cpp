@@ -95,7 +95,7 @@ struct mhpc_handle {
 static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
   sp.P = desc.n_wb + desc.n_fb;
   sp.n_wb = desc.n_wb;
-  int ko = 0, items = 0;
+  int ko = 0, items = 0, items_v = 0;
   for (int p = 0; p < sp.P; ++p) {
     const bool wb = p < desc.n_wb;
     sp.mode[p] = desc.mode_seq[p];
@@ -105,11 +105,18 @@ static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
     sp.dt[p] = wb ? desc.dt_wb : desc.dt_fb;
     ko += desc.N[p];
     sp.par_item_off[p] = items;
-    if (wb) items += (desc.N[p] - 1) * 18 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
+    sp.par_v_off[p] = items_v;
+    if (wb) {
+      items += (desc.N[p] - 1) * 7 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
+      items_v += (desc.N[p] - 1) * 11;
+    }
   }
-  sp.par_item_off[sp.P] = items;
-  for (int p = sp.P + 1; p <= MAXP; ++p) sp.par_item_off[p] = items;
+  for (int p = sp.P; p <= MAXP; ++p) {
+    sp.par_item_off[p] = items;
+    sp.par_v_off[p] = items_v;
+  }
   sp.par_items = items;
+  sp.par_items_v = items_v;
   sp.NK = ko;
 }
 

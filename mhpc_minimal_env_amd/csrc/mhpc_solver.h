@@ -51,8 +51,10 @@ struct SolveParams {
   double eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
   int AL_active, ReB_active;
   int buf[MAXP];             // phase buffer of each phase (receding horizon, see k_store_*)
-  int par_items;             // partials work items per problem
-  int par_item_off[MAXP + 1];  // prefix offsets of partials items per phase
+  // partials work items per problem and their prefix offsets per phase, in two classes:
+  // configuration directions (+ the impact directions) and velocity / control directions
+  int par_items, par_items_v;
+  int par_item_off[MAXP + 1], par_v_off[MAXP + 1];
 };
 
 struct ProbState {
