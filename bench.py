@@ -145,9 +145,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="problems per GPU (default: c3 1024, c5 4096, c2 1)")
-    ap.add_argument("--workload", choices=["c3", "c5", "c2"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c5", "c5f32", "c2"], default="c3",
                     help="c3: the headline 2WB+2SRB solve (BASELINE configs[2]); c5: 4WB+6SRB "
-                         "bound solve; c2: 256 trial rollouts of one nominal per problem")
+                         "bound solve (fp64), c5f32: the same in the fp32 instantiation "
+                         "(BASELINE configs[4]); c2: 256 trial rollouts of one nominal per problem")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="CPU-baseline problems (default: c3 16384, c5 8192)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -170,7 +171,7 @@ def main():
     from mhpc_minimal_env_amd import capi, configs
     from mhpc_minimal_env_amd import locomotion as L
 
-    B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c2": 1}[args.workload]
+    B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c5f32": 4096, "c2": 1}[args.workload]
     desc, opt = getattr(configs, f"{args.workload}_desc")(), L.HSDDP_OPTION()
     x0 = configs.x0_for(desc, B, offset=rank * B)
     if args.workload == "c2":
@@ -237,10 +238,11 @@ def main():
             cpu, why = cpu_baseline(desc, opt, args.cpu_sample or
                                     (16384 if args.workload == "c3" else 8192),
                                     min(args.cpu_threads, os.cpu_count() or 1),
-                                    label=args.workload.upper())
+                                    label=args.workload.upper()[:2])
         line = {
             "metric": ("MHPC solves/sec (2WB+2SRB trot)" if args.workload == "c3"
-                       else "MHPC solves/sec (4WB+6SRB bound)"),
+                       else "MHPC solves/sec (4WB+6SRB bound)"
+                       + (", fp32" if args.workload == "c5f32" else "")),
             "value": total / dt,
             "unit": "solves/s",
             "n_gpus": world,
@@ -250,7 +252,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if args.workload == "c5f32" else "f64",
             "data": "synthetic (x0 = reference default + splitmix64 perturbation)",
             "config": {
                 "workload": (("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, "

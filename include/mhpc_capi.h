@@ -69,7 +69,9 @@ typedef struct {
   double dt_fb;
   double vel_cmd;     /* USRCMD::vel (float promoted) */
   double height_cmd;  /* USRCMD::height */
-  int32_t precision;  /* 64 (fp32 is a later extension; 32 is rejected for now) */
+  int32_t precision;  /* 64: fp64 (the reference's MHPCLocomotion<double>); 32: the fp32
+                       * instantiation of the same kernels (config C5).  Host arrays at
+                       * the ABI stay double in both cases. */
   int32_t reserved;
 } mhpc_problem_desc;
 

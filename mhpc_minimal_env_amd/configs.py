@@ -5,7 +5,7 @@ C2  1 WB phase (mode 1), dt_wb = (float)(0.08f/120), N = 120
 C3  2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(GaitType2D::PRONK) = default branch,
     uniform 0.08 s, dt = (float)0.001 -> N = 80 each; "trot" in BASELINE.json
 C4  = C3, sharded over GPUs
-C5  Gait() BOUND, 4 WB + 6 SRB (fp32 in BASELINE.json; fp64 here until the fp32 path lands)
+C5  Gait() BOUND, 4 WB + 6 SRB; c5f32_desc() runs it in the fp32 instantiation (BASELINE.json)
 demo  test_main.cpp: default MHPCUserParameters (4 WB + 4 SRB), Gait() BOUND, default x0
 """
 from __future__ import annotations
@@ -31,9 +31,16 @@ def c3_desc():
     return L.desc_from_params(params, L.Gait(L.GaitType2D.PRONK))
 
 
-def c5_desc():
+def c5_desc(precision: int = 64):
     params = L.MHPCUserParameters(n_wbphase=4, n_fbphase=6, usrcmd=L.USRCMD(vel=1.5))
-    return L.desc_from_params(params, L.Gait())
+    d = L.desc_from_params(params, L.Gait())
+    d.precision = precision
+    return d
+
+
+def c5f32_desc():
+    """C5 in the fp32 instantiation of the solve path (BASELINE.json configs[4])."""
+    return c5_desc(32)
 
 
 def demo_desc():

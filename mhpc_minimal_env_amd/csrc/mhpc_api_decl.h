@@ -1,0 +1,25 @@
+// Per-precision implementation of the C-ABI (mhpc_runtime.cpp compiled once per arithmetic
+// type into namespace API_NS); mhpc_capi.cpp exports the extern "C" symbols and dispatches
+// on the descriptor's precision.  No include guard: included once per namespace.
+namespace API_NS {
+struct Handle;
+const char* api_kernel_name(int k);
+int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int batch, int device,
+               Handle** out);
+int api_set_x0(Handle* h, const double* x0);
+int api_initialize(Handle* h);
+int api_solve(Handle* h, int32_t* status);
+int api_get_phase(Handle* h, int phase, double* x, double* u, double* y, double* K, double* du,
+                  double* Vx);
+int api_get_scalars(Handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
+                    double* dV_phase, int32_t* trace);
+int api_rollout_costs(Handle* h, int n_eps, const double* eps, double* J, double* viol, float* ms);
+int api_get_cost_gradients(Handle* h, int phase, double* lx, double* Phix);
+int api_update_problem(Handle* h, const mhpc_gait* gait);
+int api_get_desc(Handle* h, mhpc_problem_desc* desc);
+int api_get_counters(Handle* h, mhpc_counters* c);
+int api_set_profiling(Handle* h, int on);
+int api_get_kernel_stats(Handle* h, double* ms, int64_t* launches, double* alg_bytes);
+int api_reset_kernel_stats(Handle* h);
+void api_destroy(Handle* h);
+}  // namespace API_NS

@@ -21,7 +21,7 @@
 
 #include "mhpc_device.h"
 
-namespace mhpc {
+namespace MHPC_NS {
 
 // Padded LDS shapes: every lane of a round runs the same straight-line code; rows / columns
 // past the real extents land in padding that no real output reads.
@@ -36,28 +36,28 @@ template <int NX> struct QShape {
 };
 
 struct BwsLds {
-  double H[196], G[14];  // value function of knot k+1, then of knot k (row stride NX)
-  double W[7 * WS];      // rows NQ..NX-1 of [A B]
-  double G2[2 * WS];     // stance rows of [C D]
-  double l[JR];          // (lx, lu)
-  double ldiag[18];      // diagonal running-cost Hessian (lxx, luu)
-  double lyy2[4], ly2[2];
+  real H[196], G[14];  // value function of knot k+1, then of knot k (row stride NX)
+  real W[7 * WS];      // rows NQ..NX-1 of [A B]
+  real G2[2 * WS];     // stance rows of [C D]
+  real l[JR];          // (lx, lu)
+  real ldiag[18];      // diagonal running-cost Hessian (lxx, luu)
+  real lyy2[4], ly2[2];
   union {
     struct {
-      double Jt[JR * 14];  // [A B]' H   (NR x NX)
-      double Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
+      real Jt[JR * 14];  // [A B]' H   (NR x NX)
+      real Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
     };
     struct {
-      double H2[196];      // impact-aware step: lifted H' and (Px' H2)
-      double Px[196];
-      double T[196];
+      real H2[196];      // impact-aware step: lifted H' and (Px' H2)
+      real Px[196];
+      real T[196];
     };
   };
-  double Qv[18];         // (Qx, Qu)
-  double xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
-  double Kst[56], dust[4], Gst[14];     // results of the last knot, stored one knot later
-  double hx[14], Hs[9], G2v[14];
-  double dV;
+  real Qv[18];         // (Qx, Qu)
+  real xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
+  real Kst[56], dust[4], Gst[14];     // results of the last knot, stored one knot later
+  real hx[14], Hs[9], G2v[14];
+  real dV;
   int fail;
 #ifdef MHPC_BWS_TIMING
   unsigned long long cyc[12], tlast;
@@ -81,8 +81,8 @@ __device__ unsigned long long g_bws_cyc[12];
 #endif
 
 // Eigen-style 4x4 inverse by cofactors (same formulas as the oracle).
-__device__ __forceinline__ void inverse4(const double* m, double* inv) {
-  double a[16];
+__device__ __forceinline__ void inverse4(const real* m, real* inv) {
+  real a[16];
   a[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] +
          m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
   a[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] -
@@ -115,7 +115,7 @@ __device__ __forceinline__ void inverse4(const double* m, double* inv) {
           m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
   a[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] +
           m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
-  const double det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
+  const real det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
 #pragma unroll
   for (int i = 0; i < 16; ++i) inv[i] = a[i] / det;
 }
@@ -126,21 +126,21 @@ __device__ __forceinline__ void inverse4(const double* m, double* inv) {
 // ZeroSign; true iff no strictly negative pivot.  Branch-free (the pivot swaps are
 // selects) so the scheduler can interleave it with the independent inverse / value-
 // function work of the same round; same arithmetic as the oracle.
-__device__ __forceinline__ void sel_swap(bool c, double& a, double& b) {
-  const double ta = a, tb = b;
+__device__ __forceinline__ void sel_swap(bool c, real& a, real& b) {
+  const real ta = a, tb = b;
   a = c ? tb : ta;
   b = c ? ta : tb;
 }
-__device__ __forceinline__ bool ldlt_is_positive4(double* A) {
+__device__ __forceinline__ bool ldlt_is_positive4(real* A) {
   int sign = 0;  // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
   bool stop = false;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     int big = k;
-    double bv = fabs(A[k * 5]);
+    real bv = fabs(A[k * 5]);
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
-      const double v = fabs(A[i * 5]);
+      const real v = fabs(A[i * 5]);
       const bool gt = v > bv;
       bv = gt ? v : bv;
       big = gt ? i : big;
@@ -157,39 +157,70 @@ __device__ __forceinline__ bool ldlt_is_positive4(double* A) {
       for (int i = k + 1; i < I; ++i) sel_swap(sw, A[i * 4 + k], A[I * 4 + i]);
     }
     if (k > 0) {
-      double temp[3];
+      real temp[3];
 #pragma unroll
       for (int j = 0; j < k; ++j) temp[j] = A[j * 5] * A[k * 4 + j];
-      double s = 0;
+      real s = 0;
 #pragma unroll
       for (int j = 0; j < k; ++j) s += A[k * 4 + j] * temp[j];
       A[k * 5] -= s;
 #pragma unroll
       for (int i = k + 1; i < 4; ++i) {
-        double t = 0;
+        real t = 0;
 #pragma unroll
         for (int j = 0; j < k; ++j) t += A[i * 4 + j] * temp[j];
         A[i * 4 + k] -= t;
       }
     }
-    const double akk = A[k * 5];
-    const bool valid = fabs(akk) > 0.0;
+    const real akk = A[k * 5];
+    const bool valid = fabs(akk) > real(0.0);
     if (k == 0) stop = !valid;  // whole diagonal zero: ZeroSign, stop
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
-      const double q = A[i * 4 + k] / akk;
+      const real q = A[i * 4 + k] / akk;
       A[i * 4 + k] = valid ? q : A[i * 4 + k];
     }
     int ns = sign;
-    if (sign == 1) ns = akk < 0.0 ? 3 : 1;
-    else if (sign == 2) ns = akk > 0.0 ? 3 : 2;
-    else if (sign == 0) ns = akk > 0.0 ? 1 : (akk < 0.0 ? 2 : 0);
+    if (sign == 1) ns = akk < real(0.0) ? 3 : 1;
+    else if (sign == 2) ns = akk > real(0.0) ? 3 : 2;
+    else if (sign == 0) ns = akk > real(0.0) ? 1 : (akk < real(0.0) ? 2 : 0);
     sign = stop ? 0 : ns;
   }
   return sign == 1 || sign == 0;
 }
 
-// Value of lane `src` (uniform) of a double held per lane: two readlanes, no LDS.
+// The verdict used by default (MHPC_BWS_PSD=1): an unpivoted LDL^T of the same matrix.
+// By Sylvester's law of inertia its pivots have the signs of the pivoted factorisation's
+// whenever no pivot is exactly zero, so the verdict is the same; a zero pivot leaves its
+// column, as in Eigen.  A quarter of the instructions of the pivoted test (no pivot search
+// or swaps, three reciprocals): -16 % backward-sweep time.  tests/test_psd_verdict.py
+// checks the agreement on PD, indefinite, rank-deficient and near-singular matrices;
+// MHPC_BWS_PSD=0 selects the pivoted restatement above.
+#ifndef MHPC_BWS_PSD
+#define MHPC_BWS_PSD 1
+#endif
+__device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
+  bool neg = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const real akk = A[k * 5];
+    neg = neg || akk < real(0.0);
+    const bool valid = akk != real(0.0);
+    const real r = real(1.0) / (valid ? akk : real(1.0));
+#pragma unroll
+    for (int i = k + 1; i < 4; ++i) {
+      const real l = A[i * 4 + k] * r;
+#pragma unroll
+      for (int j = k + 1; j <= i; ++j) A[i * 4 + j] -= valid ? l * A[j * 4 + k] : real(0.0);
+    }
+  }
+  return !neg;
+}
+
+// Value of lane `src` (uniform) of a value held per lane: readlanes, no LDS.
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
 __device__ __forceinline__ double lane_bcast(double v, int src) {
   const long long b = __double_as_longlong(v);
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
@@ -199,8 +230,8 @@ __device__ __forceinline__ double lane_bcast(double v, int src) {
 
 // Row coefficient of the exact part of [A B] (see file header).
 template <int NQ>
-__device__ __forceinline__ double coef_a(int col, double dt) {
-  return col < NQ ? 1.0 : (col < 2 * NQ ? dt : 0.0);
+__device__ __forceinline__ real coef_a(int col, real dt) {
+  return col < NQ ? real(1.0) : (col < 2 * NQ ? dt : real(0.0));
 }
 template <int NQ>
 __device__ __forceinline__ int coef_b(int col) {
@@ -225,7 +256,7 @@ constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
 // (stores of the previous knot, prefetch of the next) and the drop of the next knot's
 // derivatives into LDS (nothing of R45 reads those arrays).
 template <int NT, int NQ, bool HAS_Y, class R2X, class R45X>
-__device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double eps9, R2X&& r2x,
+__device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9, R2X&& r2x,
                              R45X&& r45x) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
   constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
@@ -237,25 +268,25 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     static_assert(GR * T2 <= JR && GR * T2 <= QR && GR * T2 <= WS, "R2 padding");
     const int j = lane % NC, g = lane / NC;
     const bool isg = j == NX;
-    const double* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
+    const real* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
     const int cs = isg ? 1 : NX;
-    double hc[NQ];
+    real hc[NQ];
 #pragma unroll
     for (int r = 0; r < NQ; ++r) hc[r] = col0[(NQ + r) * cs];
     constexpr int C = T2 < CH2 ? T2 : CH2;
 #pragma unroll 1
     for (int t0 = 0; t0 < T2; t0 += C) {
-      double acc[C];
+      real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
         const int row = g + GR * (t0 + u);  // < JR
-        const double a = coef_a<NQ>(row, dt);
-        const double hb = col0[coef_b<NQ>(row) * cs];
-        double sacc = a != 0.0 ? a * hb : 0.0;
+        const real a = coef_a<NQ>(row, dt);
+        const real hb = col0[coef_b<NQ>(row) * cs];
+        real sacc = a != real(0.0) ? a * hb : real(0.0);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) sacc += sh.W[r * WS + row] * hc[r];
         if (isg) {
-          double tt = 0.0;
+          real tt = real(0.0);
           if (HAS_Y) tt = sh.G2[row] * sh.ly2[0] + sh.G2[WS + row] * sh.ly2[1];
           sacc = (sh.l[row] + sacc) + tt;
         }
@@ -270,7 +301,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
   }
   r2x();
   __syncthreads();
-  BWS_TMARK(sh, lane, 1);
+  BWS_TMARK(sh, lane, NQ == 3 ? 8 : 1);
   // R3: Qxx = (lxx + C'lyy C) + A'HA ; Qux = (0 + D'lyy C) + B'HA ; Quu = (luu + D'lyy D) + B'HB
   // (+ reg on the diagonal).  Lane = (row of Jt, column group g), the row Jt[row, NQ..] in
   // registers, T3 independent column chains.
@@ -278,33 +309,33 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     constexpr int RG = NT / NR, T3 = (NR + RG - 1) / RG;  // columns g + RG t < QV
     static_assert(RG * T3 <= QV && RG * T3 <= WS, "R3 padding");
     const int row = lane % NR, g = lane / NR;
-    double jr[NQ];
+    real jr[NQ];
 #pragma unroll
     for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
-    double c0 = 0.0, c1 = 0.0;
+    real c0 = real(0.0), c1 = real(0.0);
     if (HAS_Y) {
-      const double gr0 = sh.G2[row], gr1 = sh.G2[WS + row];
+      const real gr0 = sh.G2[row], gr1 = sh.G2[WS + row];
       c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
       c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
     }
-    const double dg = sh.ldiag[row];
+    const real dg = sh.ldiag[row];
     constexpr int C = T3 < CH3 ? T3 : CH3;
 #pragma unroll 1
     for (int t0 = 0; t0 < T3; t0 += C) {
-      double acc[C];
+      real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
         const int col = g + RG * (t0 + u);
-        const double a = coef_a<NQ>(col, dt);
-        const double jb = sh.Jt[row * NX + coef_b<NQ>(col)];
-        double sacc = a != 0.0 ? a * jb : 0.0;
+        const real a = coef_a<NQ>(col, dt);
+        const real jb = sh.Jt[row * NX + coef_b<NQ>(col)];
+        real sacc = a != real(0.0) ? a * jb : real(0.0);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * WS + col];
-        const double base = row == col ? dg : 0.0;
-        double e2 = 0.0;
+        const real base = row == col ? dg : real(0.0);
+        real e2 = real(0.0);
         if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[WS + col];
-        double v = (base + e2) + sacc;
-        if (row == col) v += 1.0 * reg;
+        real v = (base + e2) + sacc;
+        if (row == col) v += real(1.0) * reg;
         acc[u] = v;
       }
 #pragma unroll
@@ -315,15 +346,15 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     }
   }
   __syncthreads();
-  BWS_TMARK(sh, lane, 2);
+  BWS_TMARK(sh, lane, NQ == 3 ? 9 : 2);
   // R45: PSD test of Quu - 1e-9 I (every lane, registers, static indices); adjugate of Quu
   // spread over lanes 0..15 (one 3x3 minor each) and broadcast back with readlane (no LDS
   // round trip); then, in the same round, tq = Qux' Quu_inv, K = -tq', du, dV and
   // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
-  double q0[4];
+  real q0[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) q0[c] = sh.Q[NX * QS + NX + c];
-  double adj = 0.0;
+  real adj = real(0.0);
   bool psd;
   {
     // the PSD verdict is applied at the end of the round: a failed knot abandons the sweep
@@ -331,30 +362,36 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     const int i = (lane >> 2) & 3, j = lane & 3;  // lanes 0..15 of every wave
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
-    const double* q = &sh.Q[NX * QS + NX];
+    const real* q = &sh.Q[NX * QS + NX];
 #define QM(r, c) q[(r) * QS + (c)]
-    const double m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
-    const double m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
-    const double m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
+    const real m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
+    const real m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
+    const real m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
 #undef QM
-    double A[16];
+    real A[16];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        A[a * 4 + c] = sh.Q[(NX + a) * QS + NX + c] - (a == c ? 1.0 * eps9 : 0.0);
+        A[a * 4 + c] = sh.Q[(NX + a) * QS + NX + c] - (a == c ? real(1.0) * eps9 : real(0.0));
+#if MHPC_BWS_PSD == 1
+    psd = ldlt_nopiv_is_positive4(A);
+#elif MHPC_BWS_PSD == 2
+    psd = A[0] > -real(1e300);  // timing experiment only: no PSD test
+#else
     psd = ldlt_is_positive4(A);
+#endif
     // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
-    const double det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
+    const real det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
                         m02 * (m10 * m21 - m11 * m20);
     adj = ((i + j) & 1) ? -det3 : det3;
   }
-  const double det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
+  const real det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
                      q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
-  const double invl = adj / det;
-  double Qi[16];
+  const real invl = adj / det;
+  real Qi[16];
   {
-    double inv[16];  // unsymmetrised inverse (uniform)
+    real inv[16];  // unsymmetrised inverse (uniform)
 #pragma unroll
     for (int e = 0; e < 16; ++e) inv[e] = lane_bcast(invl, e);
 #pragma unroll
@@ -362,10 +399,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
 #pragma unroll
       for (int c = 0; c < 4; ++c) Qi[a * 4 + c] = (inv[a * 4 + c] + inv[c * 4 + a]) / 2;
     // dV += -Qu' inv Qu, unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
-    double s = 0;
+    real s = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      double t = 0;
+      real t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
       s += t * sh.Q[(NX + c) * QS + QV];
@@ -379,13 +416,13 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     constexpr int NI = NX + 1, GC = NT / NI, T5 = (NX + 1 + GC - 1) / GC;
     const int i = lane % NI, g = lane / NI;
     const int si = i < NX ? i : QV;
-    double qi[4];
+    real qi[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) qi[k] = sh.Q[(NX + k) * QS + si];
-    double tq[4];
+    real tq[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      double t = 0;
+      real t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
       tq[c] = t;
@@ -397,17 +434,17 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
     constexpr int C = T5 < CH5 ? T5 : CH5;
 #pragma unroll 1
     for (int t0 = 0; t0 < T5; t0 += C) {
-      double acc[C];
+      real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
         const int j = g + GC * (t0 + u);
         const int sj = j < NX ? j : QV;
-        double sacc = 0;
+        real sacc = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) sacc += tq[c] * sh.Q[(NX + c) * QS + sj];
-        const double qij = sh.Q[i * QS + sj];
-        const double qji = sh.Q[(j < NX ? j : 0) * QS + i];
-        const double base = j < NX ? (qij + qji) / 2 : qij;
+        const real qij = sh.Q[i * QS + sj];
+        const real qji = sh.Q[(j < NX ? j : 0) * QS + i];
+        const real base = j < NX ? (qij + qji) / 2 : qij;
         acc[u] = base - sacc;
       }
 #pragma unroll
@@ -420,7 +457,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
   }
   r45x();
   __syncthreads();
-  BWS_TMARK(sh, lane, 7);
+  BWS_TMARK(sh, lane, NQ == 3 ? 10 : 7);
   return psd;
 }
 
@@ -430,40 +467,40 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, double dt, double reg, double
 // lane-indexed __constant__ read inside the knot loop is a vector memory load whose wait
 // would also drain the knot's prefetch and stores.
 struct CostXConsts {
-  double w2;   // 2 dt Q[i]
-  double rx;   // reference of state i (unused for i = 0: the position reference)
+  real w2;   // 2 dt Q[i]
+  real rx;   // reference of state i (unused for i = 0: the position reference)
 };
-__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, double dt) {
-  CostXConsts c{0.0, 0.0};
+__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, real dt) {
+  CostXConsts c{real(0.0), real(0.0)};
   if (lane < 14) {
     const int i = lane;
-    c.rx = i == 1 ? sp.height : i == 2 ? 0.0 : (i >= 3 && i < 7) ? cQjointBias[i - 3]
-           : i == 7 ? sp.vel : 0.0;
+    c.rx = i == 1 ? sp.height : i == 2 ? real(0.0) : (i >= 3 && i < 7) ? cQjointBias[i - 3]
+           : i == 7 ? sp.vel : real(0.0);
     c.w2 = 2 * dt * cQwb[i];
   }
   return c;
 }
-__device__ __forceinline__ void wb_cost_x(BwsLds& sh, int lane, const CostXConsts& c, double pos) {
+__device__ __forceinline__ void wb_cost_x(BwsLds& sh, int lane, const CostXConsts& c, real pos) {
   if (lane < 14) {
-    const double rxi = lane == 0 ? pos : c.rx;
+    const real rxi = lane == 0 ? pos : c.rx;
     sh.l[lane] = c.w2 * (sh.xb[lane] - rxi);
     sh.ldiag[lane] = c.w2;
   }
 }
 
 // SRB Jacobian entry of row 3+r, column col of [A B] (FBDynamics_par.c operation order).
-__device__ __forceinline__ double srb_w_entry(int r, int col, const double* x, const double* u,
-                                              const double* p, const double* s, double dt) {
+__device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const real* u,
+                                              const real* p, const real* s, real dt) {
   MHPC_NO_FMA
   const int row = 3 + r;
-  double ac = 0.0;
+  real ac = real(0.0);
   if (col < 6) {
     if (row == 5 && col == 0) ac = s[0] * (kSrbInvInertia * u[1]) + s[1] * (kSrbInvInertia * u[3]);
     if (row == 5 && col == 1) ac = -(s[0] * (kSrbInvInertia * u[0]) + s[1] * (kSrbInvInertia * u[2]));
-    return (col == row ? 1.0 : 0.0) + ac * dt;
+    return (col == row ? real(1.0) : real(0.0)) + ac * dt;
   }
   const int c = col - 6;
-  double bc = 0.0;
+  real bc = real(0.0);
   if (row == 3 && c == 0) bc = kSrbInvMass * s[0];
   if (row == 5 && c == 0) bc = s[0] * (kSrbInvInertia * (p[1] - x[1]));
   if (row == 4 && c == 1) bc = kSrbInvMass * s[0];
@@ -480,13 +517,13 @@ __device__ __forceinline__ double srb_w_entry(int r, int col, const double* x, c
 // (quirk B1: forward_sweep_partials_only does not add them).
 template <int NT, int NX>
 __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLds& sh, int lane,
-                               int p, double pos, const double* xe, double* Gout) {
+                               int p, real pos, const real* xe, real* Gout) {
   constexpr bool wb = NX == 14;
   const int mode = sp.mode[p];
   const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
-  double h = 0;
+  real h = 0;
   if (al && lane == 0) {
-    double hx[14], Hs[3][3];
+    real hx[14], Hs[3][3];
     if (mode == 2) wb_touchdown_compact<kFront>(xe, &h, hx, Hs);
     else wb_touchdown_compact<kBack>(xe, &h, hx, Hs);
 #pragma unroll
@@ -497,28 +534,28 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
   }
   __syncthreads();
   if (al) h = sh.G2v[0];
-  const double s = st->sigma[p], lam = st->lambda[p];
+  const real s = st->sigma[p], lam = st->lambda[p];
   const int ih = mode == 2 ? 3 : 5;  // touchdown Hessian block (theta, hip, knee)
   #pragma unroll 1
   for (int e = lane; e < NX * NX + NX; e += NT) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
-      double v = i == j ? (wb ? cQfwb[mode - 1][i] : cQffb[i]) : 0.0;
+      real v = i == j ? (wb ? cQfwb[mode - 1][i] : cQffb[i]) : real(0.0);
       if (al) {
         const int ai = i == 2 ? 0 : (i == ih ? 1 : (i == ih + 1 ? 2 : -1));
         const int aj = j == 2 ? 0 : (j == ih ? 1 : (j == ih + 1 ? 2 : -1));
-        const double hij = (ai >= 0 && aj >= 0) ? sh.Hs[ai * 3 + aj] : 0.0;
+        const real hij = (ai >= 0 && aj >= 0) ? sh.Hs[ai * 3 + aj] : real(0.0);
         v += 50 * (s * s / 2 * (sh.hx[i] * sh.hx[j] + h * hij) + lam * hij);
       }
       sh.H[e] = v + sh.H[e];
     } else {
       const int i = e - NX * NX;
-      double rxi;
+      real rxi;
       if (wb) rxi = i == 0 ? pos : (i == 7 ? sp.vel : cXtermWB[mode - 1][i]);
-      else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : 0.0));
-      double v = (wb ? cQfwb[mode - 1][i] : cQffb[i]) * (xe[i] - rxi);
+      else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : real(0.0)));
+      real v = (wb ? cQfwb[mode - 1][i] : cQffb[i]) * (xe[i] - rxi);
       if (al) v += 50 * (s * s / 2 * sh.hx[i] * h + lam * sh.hx[i]);
-      const double g = v + sh.G[i];
+      const real g = v + sh.G[i];
       sh.G[i] = g;
       Gout[i] = g;
     }
@@ -539,27 +576,27 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
   for (int e = lane; e < 196 + 14; e += NT) {
     if (e < 196) {
       const int i = e / 14, j = e - i * 14;
-      double v;
+      real v;
       if (nwb) v = sh.H[e];
       else {
         const int pi = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
         const int pj = j < 3 ? j : (j >= 7 && j < 10 ? j - 4 : -1);
-        v = (pi >= 0 && pj >= 0) ? sh.H[pi * 6 + pj] : 0.0;
+        v = (pi >= 0 && pj >= 0) ? sh.H[pi * 6 + pj] : real(0.0);
       }
       sh.H2[e] = v;
     } else {
       const int i = e - 196;
-      double v;
+      real v;
       if (nwb) v = sh.G[i];
       else {
         const int q = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
-        v = q >= 0 ? sh.G[q] : 0.0;
+        v = q >= 0 ? sh.G[q] : real(0.0);
       }
       sh.G2v[i] = v;
     }
   }
   if (imp) {
-    const double* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
+    const real* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
     #pragma unroll 1
     for (int e = lane; e < 196; e += NT) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
     if (lane == 0) ++*px_reads;
@@ -571,13 +608,13 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
     for (int e = lane; e < 196 + 14; e += NT) {
       if (e < 196) {
         const int i = e / 14, j = e - i * 14;
-        double s = 0;
+        real s = 0;
 #pragma unroll
         for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.H2[m * 14 + j];
         sh.T[e] = s;
       } else {
         const int i = e - 196;
-        double s = 0;
+        real s = 0;
 #pragma unroll
         for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.G2v[m];
         sh.G[i] = s;
@@ -587,7 +624,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
     #pragma unroll 1
     for (int e = lane; e < 196; e += NT) {
       const int i = e / 14, j = e - i * 14;
-      double s = 0;
+      real s = 0;
 #pragma unroll
       for (int m = 0; m < 14; ++m) s += sh.T[i * 14 + m] * sh.Px[m * 14 + j];
       sh.H[e] = s;
@@ -610,6 +647,9 @@ constexpr int kVmcnt0 = 0x0F70;
 template <int NT, int NX>
 __device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const BwsLds& sh,
                                            int lane) {
+#ifdef MHPC_BWS_NOSTORE
+  return;  // timing experiment only
+#endif
 #pragma unroll
   for (int t = 0; t < (5 * NX + 4 + NT - 1) / NT; ++t) {
     const int e = lane + NT * t;
@@ -624,23 +664,23 @@ __device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const B
 // one loop per variant keeps each variant's hoisted lane addresses out of the other's.
 template <int NT, bool STANCE>
 __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
-                               BwsLds& sh, int lane, int p, double reg, int64_t* knots) {
+                               BwsLds& sh, int lane, int p, real reg, int64_t* knots) {
   const int N = sp.N[p], ko = sp.ko[p];
-  const double dt = sp.dt[p];
+  const real dt = sp.dt[p];
   const int nom = st->nom_slot;
   constexpr bool stance = STANCE;
-  const double* pos = d.refpos + (size_t)b * sp.NK + ko;
+  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   // prefetch registers: PT doubles of the partials record + 1 of the nominal knot
   constexpr int PT = (PS + NT - 1) / NT;
-  double pre[PT], prex = 0;
+  real pre[PT], prex = 0;
   auto load = [&](int k) {
-    const double* prec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+    const real* prec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int e = lane + NT * t;
       pre[t] = prec[e < PS ? e : PS - 1];  // unconditional: no exec-masked load
     }
-    const double* tk = traj_ptr(sp, d, b, nom, ko + k);
+    const real* tk = traj_ptr(sp, d, b, nom, ko + k);
     prex = *(lane < 22 ? tk + lane : lane == 22 ? pos + k : tk);
   };
   const CostXConsts cx = wb_cost_x_consts(lane, sp, dt);
@@ -654,7 +694,7 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
       const int e = lane + NT * t;
       if (e < PS_JAC) {
         const int col = e / 9, r = e - col * 9;
-        if (r < 7) sh.W[r * WS + col] = (col == 7 + r ? 1.0 : 0.0) + pre[t] * dt;
+        if (r < 7) sh.W[r * WS + col] = (col == 7 + r ? real(1.0) : real(0.0)) + pre[t] * dt;
         else if (stance) sh.G2[(r - 7) * WS + col] = pre[t];
       } else if (e < PS) {
         const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
@@ -664,9 +704,9 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
         else sh.lyy2[q - 10] = pre[t];
       }
     }
-    const double pk = lane_bcast(prex, 22);
+    const real pk = lane_bcast(prex, 22);
     if (lane < 14) {
-      const double rxi = lane == 0 ? pk : cx.rx;
+      const real rxi = lane == 0 ? pk : cx.rx;
       sh.l[lane] = cx.w2 * (prex - rxi);
       sh.ldiag[lane] = cx.w2;
     }
@@ -693,46 +733,46 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
 
 template <int NT>
 __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
-                               BwsLds& sh, int lane, int p, double reg, int64_t* knots) {
+                               BwsLds& sh, int lane, int p, real reg, int64_t* knots) {
   const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const double dt = sp.dt[p];
+  const real dt = sp.dt[p];
   const int nom = st->nom_slot;
-  const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-  double foot[4], cs[2];
+  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
+  real foot[4], cs[2];
   plan_foothold(traj_ptr(sp, d, b, nom, ko), dt * N, mode, foot);
   srb_contact(mode, cs);
   const int m = mode - 1;
   // per-lane cost weight 2 dt Q (lanes 30..35: state i) / 2 dt R (lanes 36..39: control c)
   // and fixed reference, hoisted out of the knot loop (see wb_cost_x_consts)
-  double fb_w2 = 0.0, fb_rx = 0.0;
+  real fb_w2 = real(0.0), fb_rx = real(0.0);
   if (lane >= 30 && lane < 36) {
     const int i = lane - 30;
     fb_w2 = 2 * dt * cQfb[i];
-    fb_rx = i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
+    fb_rx = i == 1 ? sp.height : i == 3 ? sp.vel : real(0.0);
   } else if (lane >= 36 && lane < 40) {
     const int c = lane - 36;
     fb_w2 = 2 * dt * cRfb[m][c];
-    fb_rx = (c == 1 || c == 3) ? 8.252 * 9.81 : 0.0;
+    fb_rx = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
   }
   auto loadx = [&](int k) {  // unconditional single load per lane (no exec-masked load)
-    const double* tk = traj_ptr(sp, d, b, nom, ko + k);
+    const real* tk = traj_ptr(sp, d, b, nom, ko + k);
     return *(lane < 10 ? tk + lane : lane == 10 ? pos + k : tk);
   };
   // drop of knot k: the nominal (x 6, u 4) and position reference sit in prex of lanes
   // 0..10; W rows (FBDynamics_par.c order) and the cost derivatives straight from registers
-  auto drop = [&](double px) {
+  auto drop = [&](real px) {
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    const double xs[2] = {lane_bcast(px, 0), lane_bcast(px, 1)};
-    const double us[4] = {lane_bcast(px, 6), lane_bcast(px, 7), lane_bcast(px, 8),
+    const real xs[2] = {lane_bcast(px, 0), lane_bcast(px, 1)};
+    const real us[4] = {lane_bcast(px, 6), lane_bcast(px, 7), lane_bcast(px, 8),
                           lane_bcast(px, 9)};
-    const double pk = lane_bcast(px, 10);
-    const double own = __shfl(px, lane >= 36 ? lane - 30 : (lane >= 30 ? lane - 30 : 0));
+    const real pk = lane_bcast(px, 10);
+    const real own = __shfl(px, lane >= 36 ? lane - 30 : (lane >= 30 ? lane - 30 : 0));
     if (lane < 30) {
       const int r = lane / 10, col = lane - r * 10;
       sh.W[r * WS + col] = srb_w_entry(r, col, xs, us, foot, cs, dt);
     } else if (lane < 36) {
       const int i = lane - 30;
-      const double rxi = i == 0 ? pk : fb_rx;
+      const real rxi = i == 0 ? pk : fb_rx;
       sh.l[i] = fb_w2 * (own - rxi);
       sh.ldiag[i] = fb_w2;
     } else if (lane < 40) {
@@ -741,7 +781,7 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
       sh.ldiag[6 + c] = fb_w2;
     }
   };
-  double prex = loadx(N - 2);
+  real prex = loadx(N - 2);
   drop(prex);
   __syncthreads();
   for (int k = N - 2; k >= 0; --k) {
@@ -763,7 +803,7 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
 
 template <int NT>
 __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st, BwsLds& sh,
-                          double reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads) {
+                          real reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads) {
   const int lane = threadIdx.x;
   const int nom = st->nom_slot;
   #pragma unroll 1
@@ -779,9 +819,9 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
       if (lane == 0) sh.dV = st->dV[p + 1];  // dVnext
     }
     __syncthreads();
-    const double* pos = d.refpos + (size_t)b * sp.NK + ko;
-    double* Gp = d.G + ((size_t)b * sp.NK + ko + N - 1) * 14;
-    const double* xe = traj_ptr(sp, d, b, nom, ko + N - 1);
+    const real* pos = d.refpos + (size_t)b * sp.NK + ko;
+    real* Gp = d.G + ((size_t)b * sp.NK + ko + N - 1) * 14;
+    const real* xe = traj_ptr(sp, d, b, nom, ko + N - 1);
     int64_t kn = 0;
     bool ok;
     if (wb) {
@@ -808,13 +848,13 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
 // register cap, widest ILP) is fastest, beyond that the 2-wave build hides latency by
 // co-residency.
 template <int NT, int WAVES>
-__global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, double update_reg) {
+__global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, real update_reg) {
   const int b = blockIdx.x;
   if (b >= sp.B) return;
   ProbState* st = &d.st[b];
   if (!(st->active && st->ddp_active)) return;
   __shared__ BwsLds sh;
-  double reg = st->reg;
+  real reg = st->reg;
   int bws_iter = 1;
   int64_t knots = 0, knots_wb = 0, px_reads = 0, sweeps = 0;
   bool aborted = false;
@@ -827,7 +867,7 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, do
   for (;;) {
     ++sweeps;
     if (bws_sweep<NT>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
-    reg = fmax(reg * update_reg, 1e-03);  // MultiPhaseDDP.cpp:218
+    reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
     ++bws_iter;
     if (reg > 1000) { aborted = true; break; }
   }
@@ -855,13 +895,13 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, do
     } else {
       st->dV_exp = st->dV[0];  // _exp_cost_change = _phases[0]->_dV
       reg = reg / 20;          // MultiPhaseDDP.cpp:237-241
-      if (reg < 1e-06) reg = 0;
+      if (reg < real(1e-06)) reg = 0;
       st->reg = reg;
     }
   }
 }
 
-hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, double update_reg, hipStream_t s) {
+hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, hipStream_t s) {
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
@@ -881,17 +921,17 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, double update_reg
   return hipGetLastError();
 }
 
-}  // namespace mhpc
+}  // namespace MHPC_NS
 
 #ifdef MHPC_BWS_TIMING
 extern "C" int mhpc_dbg_bws_cycles(unsigned long long* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mhpc::g_bws_cyc), sizeof(unsigned long long) * 12) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_bws_cyc), sizeof(unsigned long long) * 12) !=
       hipSuccess)
     return 1;
   if (reset) {
     unsigned long long z[12] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(mhpc::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
   }
   return 0;
 }

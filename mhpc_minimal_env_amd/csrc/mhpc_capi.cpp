@@ -1,0 +1,113 @@
+// The exported C-ABI (include/mhpc_capi.h): one handle type for both arithmetic types; every
+// call forwards to the fp64 (namespace mhpc) or fp32 (namespace mhpc32) instantiation of
+// mhpc_runtime.cpp according to the descriptor's precision at mhpc_create.
+#include <math.h>
+
+#include <string>
+
+#include "../../include/mhpc_capi.h"
+
+thread_local std::string mhpc_g_err;
+
+#define API_NS mhpc
+#include "mhpc_api_decl.h"
+#undef API_NS
+#define API_NS mhpc32
+#include "mhpc_api_decl.h"
+#undef API_NS
+
+struct mhpc_handle {
+  int precision;
+  void* impl;
+};
+
+#define FWD(fn, ...)                                                                 \
+  do {                                                                               \
+    if (!h) {                                                                        \
+      mhpc_g_err = "null handle";                                                    \
+      return MHPC_ERR_INVALID;                                                       \
+    }                                                                                \
+    return h->precision == 32 ? mhpc32::api_##fn((mhpc32::Handle*)h->impl, ##__VA_ARGS__) \
+                              : mhpc::api_##fn((mhpc::Handle*)h->impl, ##__VA_ARGS__);   \
+  } while (0)
+
+extern "C" const char* mhpc_version(void) {
+  return "mhpc_minimal_env_amd 0.2 (gfx950; fp64 and fp32 solve paths)";
+}
+extern "C" const char* mhpc_last_error(void) { return mhpc_g_err.c_str(); }
+extern "C" const char* mhpc_kernel_name(int k) { return mhpc::api_kernel_name(k); }
+
+extern "C" int mhpc_phase_dims(const mhpc_problem_desc* desc, int phase, int* xsize, int* N) {
+  if (!desc) {
+    mhpc_g_err = "null descriptor";
+    return MHPC_ERR_INVALID;
+  }
+  const int P = desc->n_wb + desc->n_fb;
+  if (phase < 0 || phase >= P || P > MHPC_MAX_PHASES) {
+    mhpc_g_err = "bad phase";
+    return MHPC_ERR_INVALID;
+  }
+  if (xsize) *xsize = phase < desc->n_wb ? 14 : 6;
+  if (N) *N = desc->N[phase];
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int batch,
+                           int device, mhpc_handle** out) {
+  if (!out || !desc) {
+    mhpc_g_err = "null argument";
+    return MHPC_ERR_INVALID;
+  }
+  *out = nullptr;
+  const int prec = desc->precision;
+  void* impl = nullptr;
+  int rc;
+  if (prec == 32) {
+    mhpc32::Handle* p = nullptr;
+    rc = mhpc32::api_create(desc, opt, batch, device, &p);
+    impl = p;
+  } else {
+    mhpc::Handle* p = nullptr;
+    rc = mhpc::api_create(desc, opt, batch, device, &p);
+    impl = p;
+  }
+  if (rc != MHPC_OK) return rc;
+  *out = new mhpc_handle{prec == 32 ? 32 : 64, impl};
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_set_x0(mhpc_handle* h, const double* x0) { FWD(set_x0, x0); }
+extern "C" int mhpc_initialize(mhpc_handle* h) { FWD(initialize); }
+extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) { FWD(solve, status); }
+extern "C" int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, double* K,
+                              double* du, double* Vx) {
+  FWD(get_phase, phase, x, u, y, K, du, Vx);
+}
+extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol,
+                                double* V_phase, double* dV_phase, int32_t* trace) {
+  FWD(get_scalars, J, dV_exp, viol, V_phase, dV_phase, trace);
+}
+extern "C" int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, double* J,
+                                  double* viol, float* ms) {
+  FWD(rollout_costs, n_eps, eps, J, viol, ms);
+}
+extern "C" int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, double* Phix) {
+  FWD(get_cost_gradients, phase, lx, Phix);
+}
+extern "C" int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait) {
+  FWD(update_problem, gait);
+}
+extern "C" int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc) { FWD(get_desc, desc); }
+extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) { FWD(get_counters, c); }
+extern "C" int mhpc_set_profiling(mhpc_handle* h, int on) { FWD(set_profiling, on); }
+extern "C" int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches,
+                                     double* alg_bytes) {
+  FWD(get_kernel_stats, ms, launches, alg_bytes);
+}
+extern "C" int mhpc_reset_kernel_stats(mhpc_handle* h) { FWD(reset_kernel_stats); }
+extern "C" void mhpc_destroy(mhpc_handle* h) {
+  if (!h) return;
+  if (h->precision == 32) mhpc32::api_destroy((mhpc32::Handle*)h->impl);
+  else mhpc::api_destroy((mhpc::Handle*)h->impl);
+  delete h;
+}

@@ -8,6 +8,8 @@
 #pragma once
 #include <math.h>
 
+#include "mhpc_real.h"
+
 #if defined(__HIPCC__)
 #define MHPC_HD __host__ __device__ __forceinline__
 #else
@@ -21,14 +23,14 @@
 #define MHPC_NO_FMA
 #endif
 
-namespace mhpc {
+namespace MHPC_NS {
 
 struct Dual {
-  double v;  // primal value
-  double d;  // directional derivative
-  MHPC_HD Dual() : v(0.0), d(0.0) {}
-  MHPC_HD Dual(double a) : v(a), d(0.0) {}
-  MHPC_HD Dual(double a, double b) : v(a), d(b) {}
+  real v;  // primal value
+  real d;  // directional derivative
+  MHPC_HD Dual() : v(real(0.0)), d(real(0.0)) {}
+  MHPC_HD Dual(real a) : v(a), d(real(0.0)) {}
+  MHPC_HD Dual(real a, real b) : v(a), d(b) {}
 };
 
 MHPC_HD Dual operator+(Dual a, Dual b) { return Dual(a.v + b.v, a.d + b.d); }
@@ -36,42 +38,86 @@ MHPC_HD Dual operator-(Dual a, Dual b) { return Dual(a.v - b.v, a.d - b.d); }
 MHPC_HD Dual operator-(Dual a) { return Dual(-a.v, -a.d); }
 MHPC_HD Dual operator*(Dual a, Dual b) { return Dual(a.v * b.v, a.d * b.v + a.v * b.d); }
 MHPC_HD Dual operator/(Dual a, Dual b) {
-  const double q = a.v / b.v;
+  const real q = a.v / b.v;
   return Dual(q, (a.d - q * b.d) / b.v);
 }
-MHPC_HD Dual operator+(Dual a, double b) { return Dual(a.v + b, a.d); }
-MHPC_HD Dual operator+(double a, Dual b) { return Dual(a + b.v, b.d); }
-MHPC_HD Dual operator-(Dual a, double b) { return Dual(a.v - b, a.d); }
-MHPC_HD Dual operator-(double a, Dual b) { return Dual(a - b.v, -b.d); }
-MHPC_HD Dual operator*(Dual a, double b) { return Dual(a.v * b, a.d * b); }
-MHPC_HD Dual operator*(double a, Dual b) { return Dual(a * b.v, a * b.d); }
-MHPC_HD Dual operator/(Dual a, double b) { return Dual(a.v / b, a.d / b); }
+MHPC_HD Dual operator+(Dual a, real b) { return Dual(a.v + b, a.d); }
+MHPC_HD Dual operator+(real a, Dual b) { return Dual(a + b.v, b.d); }
+MHPC_HD Dual operator-(Dual a, real b) { return Dual(a.v - b, a.d); }
+MHPC_HD Dual operator-(real a, Dual b) { return Dual(a - b.v, -b.d); }
+MHPC_HD Dual operator*(Dual a, real b) { return Dual(a.v * b, a.d * b); }
+MHPC_HD Dual operator*(real a, Dual b) { return Dual(a * b.v, a * b.d); }
+MHPC_HD Dual operator/(Dual a, real b) { return Dual(a.v / b, a.d / b); }
 MHPC_HD Dual& operator+=(Dual& a, Dual b) { a = a + b; return a; }
 MHPC_HD Dual& operator-=(Dual& a, Dual b) { a = a - b; return a; }
 MHPC_HD Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
 
-// Scalar-generic elementary functions (double and Dual share the model source).
-MHPC_HD double val(double a) { return a; }
-MHPC_HD double val(Dual a) { return a.v; }
+// Scalar-generic elementary functions (real and Dual share the model source).
+MHPC_HD real val(real a) { return a; }
+MHPC_HD real val(Dual a) { return a.v; }
 
-MHPC_HD void sin_cos(double a, double* s, double* c) {
+#ifndef MHPC_FP32
+// sin and cos of a link angle: one Cody-Waite reduction by pi/2 (two-part pi/2, FMA) and
+// the fdlibm kernels on |r| <= pi/4 (< 0.75 ulp each); <= 1.5 ulp overall, checked against
+// long double on |a| <= 60.  About half the instructions of the library sincos, whose
+// reduction carries a double-double and a Payne-Hanek path for huge arguments -- kept here
+// only for |a| > 1e5 (a diverged rollout), where the short reduction loses accuracy.
+MHPC_HD void sin_cos_short(double a, double* s, double* c) {
+  const double k = rint(a * 0.63661977236758138);              // 2 / pi
+  double r = fma(-k, 1.5707963267948966, a);                   // pi/2, high part
+  r = fma(-k, 6.123233995736766e-17, r);                       // pi/2 - high part
+  const double z = r * r;
+  const double ps = 8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 +
+                         z * (2.75573137070700676789e-06 +
+                              z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+  const double sn = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
+  const double pc =
+      z * (4.16666666666666019037e-02 +
+           z * (-1.38888888888741095749e-03 +
+                z * (2.48015872894767294178e-05 +
+                     z * (-2.75573143513906633035e-07 +
+                          z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cs = w + (((1.0 - w) - hz) + z * pc);
+  const int n = (int)k & 3;
+  const double so = (n & 1) ? cs : sn, co = (n & 1) ? sn : cs;
+  *s = (n & 2) ? -so : so;
+  *c = ((n + 1) & 2) ? -co : co;
+}
+#endif
+
+MHPC_HD void sin_cos(real a, real* s, real* c) {
+#ifdef MHPC_FP32
 #if defined(__HIP_DEVICE_COMPILE__)
-  sincos(a, s, c);  // one shared argument reduction on the device
+  sincosf(a, s, c);
 #else
-  *s = sin(a);
-  *c = cos(a);
+  *s = sinf(a);
+  *c = cosf(a);
+#endif
+#else
+  if (fabs(a) <= 1e5) {
+    sin_cos_short(a, s, c);
+  } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincos(a, s, c);
+#else
+    *s = sin(a);
+    *c = cos(a);
+#endif
+  }
 #endif
 }
 MHPC_HD void sin_cos(Dual a, Dual* s, Dual* c) {
-  double sv, cv;
+  real sv, cv;
   sin_cos(a.v, &sv, &cv);
   *s = Dual(sv, cv * a.d);
   *c = Dual(cv, -sv * a.d);
 }
-MHPC_HD double sqrt_(double a) { return sqrt(a); }
+MHPC_HD real sqrt_(real a) { return sqrt(a); }
 MHPC_HD Dual sqrt_(Dual a) {
-  const double r = sqrt(a.v);
-  return Dual(r, a.d / (2.0 * r));
+  const real r = sqrt(a.v);
+  return Dual(r, a.d / (real(2.0) * r));
 }
 
-}  // namespace mhpc
+}  // namespace MHPC_NS

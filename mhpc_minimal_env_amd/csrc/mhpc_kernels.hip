@@ -22,7 +22,7 @@
 
 #include "mhpc_device.h"
 
-namespace mhpc {
+namespace MHPC_NS {
 
 // ============================================================================================
 // k_rollout: forward_iteration (MultiPhaseDDP.cpp:130-151) -- every Armijo trial at once.
@@ -36,7 +36,24 @@ namespace mhpc {
 // One barrier per knot hands the ring over; the cost and the scattered stores leave the
 // dynamics chain.  At the end the first accepted trial of each problem is selected in-block.
 // ============================================================================================
-constexpr int RING_W = 22;  // doubles per ring record (x 14, u 4, y 4)
+constexpr int RING_W = 22;  // reals per ring record (x 14, u 4, y 4)
+#ifdef MHPC_FP32
+using real2 = float2;
+#else
+using real2 = double2;
+#endif
+
+// Optional cycle accounting of the rollout's knot loop (build with -DMHPC_RO_TIMING, read
+// with mhpc_dbg_ro_cycles; lane 0 of the dynamics wave of every block): 0 WB feedback u,
+// 1 WB dynamics, 2 WB record hand-over (ring + barrier), 3 SRB knot, 4 / 5 WB / SRB knots.
+#ifdef MHPC_RO_TIMING
+__device__ unsigned long long g_ro_cyc[6];
+#define RO_T(v) const unsigned long long v = (lane == 0 && w0) ? clock64() : 0ull
+#define RO_ADD(i, v) do { if (lane == 0 && w0) ro_cyc[i] += (v); } while (0)
+#else
+#define RO_T(v) do { } while (0)
+#define RO_ADD(i, v) do { } while (0)
+#endif
 
 // PIPE = false: the same wave plays both roles (no ring, registers hand over) -- better
 // once the batch fills the chip, when a second wave per block only competes for issue.
@@ -55,9 +72,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   const int b = blockIdx.x * ppw + lp;
   const bool in = lp < ppw && b < sp.B;
 
-  __shared__ double ring[PIPE ? 2 : 1][RING_W][64];
-  __shared__ double sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
+  __shared__ real ring[PIPE ? 2 : 1][RING_W][64];
+  __shared__ real sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
   __shared__ int sAny;
+#ifdef MHPC_RO_TIMING
+  unsigned long long ro_cyc[6] = {0, 0, 0, 0, 0, 0};
+#endif
 
   if (t == 0) sAny = 0;
   __syncthreads();
@@ -75,60 +95,70 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   if (!sAny) return;  // uniform: no problem of this block is still iterating
   if (full && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
     if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
-    const bool reb_off = (st->viol > 0.05) || al_iter == 1;
+    const bool reb_off = (st->viol > real(0.05)) || al_iter == 1;
     st->reb_active = (st->cap_reb && !reb_off) ? 1 : 0;
     st->opt_reb = st->reb_active;
   }
   if (full) __syncthreads();
 
-  const double eps = run && !full ? sp.eps[j] : 0.0;
+  const real eps = run && !full ? sp.eps[j] : real(0.0);
   const bool reb = run && st->reb_active;
-  double x[14];
+  real x[14];
   if (w0 && run) {
-    const double* x0 = d.x0 + (size_t)b * 14;
+    const real* x0 = d.x0 + (size_t)b * 14;
     for (int i = 0; i < 14; ++i) x[i] = x0[i];
   }
-  double J = 0, viol2 = 0;
+  real J = 0, viol2 = 0;
   int q = 0;  // ring records handed over so far
-  // wave 1: store the lane's ring record (n doubles, n even) to knot kk of its slot with
-  // 16-byte stores (records are 16-byte aligned: KS * 8 = 192)
-  auto store_rec = [&](const double* r, int n, int kk) {
-    double2* o = reinterpret_cast<double2*>(traj_ptr(sp, d, b, slot, kk));
+  // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
+  // 2-wide stores (records are aligned to them: KS * sizeof(real))
+  auto store_rec = [&](const real* r, int n, int kk) {
+    real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
     for (int i = 0; i < RING_W / 2; ++i)
-      if (2 * i < n) o[i] = make_double2(r[2 * i], r[2 * i + 1]);
+      if (2 * i < n) o[i] = real2{r[2 * i], r[2 * i + 1]};
   };
   for (int p = 0; p < sp.P; ++p) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const double dt = sp.dt[p];
+    const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
     const int nx = wb ? 14 : 6, nrec = wb ? RING_W : 14;
-    double V = 0, delta = 0, etq = 0, egr = 0;
+    real V = 0, delta = 0, etq = 0, egr = 0;
     if (w1 && run && wb) { delta = st->delta[p]; etq = st->eps_tq[p]; egr = st->eps_grf[p]; }
-    double f[4], sc[2];
+    real f[4], sc[2];
     if (w0 && run && !wb) {
       plan_foothold(x, dt * N, mode, f);
       srb_contact(mode, sc);
     }
-    const double* refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
+    const real* refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
     for (int k = 0; k < N - 1; ++k, ++q) {
       const int s = PIPE ? (q & 1) : 0;
-      double rr[RING_W];
+      real rr[RING_W];
+      RO_T(tk0);
+#ifdef MHPC_RO_TIMING
+      unsigned long long tk1 = 0, tk2 = 0;
+#endif
       if (w0 && run) {
-        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        const real* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const real* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const real* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
         if (wb) {
-          double u[4];
+          real u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            double fb = 0;
+            real fb = 0;
 #pragma unroll
             for (int c = 0; c < 14; ++c) fb += Kk[i * 14 + c] * (x[c] - nk[c]);
             u[i] = (nk[14 + i] + eps * duk[i]) + fb;
           }
-          double xd[14], y[4];
-          wb_dynamics<double>(x, u, mode, xd, y);
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk1 = clock64();
+#endif
+          real xd[14], y[4];
+          wb_dynamics<real>(x, u, mode, xd, y);
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk2 = clock64() + 0 * xd[13];
+#endif
 #pragma unroll
           for (int i = 0; i < 14; ++i) rr[i] = x[i];
 #pragma unroll
@@ -136,20 +166,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 #pragma unroll
           for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
         } else {
-          double u[4];
+          real u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            double fb = 0;
+            real fb = 0;
 #pragma unroll
             for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
             u[i] = (nk[6 + i] + eps * duk[i]) + fb;
           }
-          double xd[6];
+          real xd[6];
           srb_dynamics(x, u, f, sc, xd);
 #pragma unroll
           for (int i = 0; i < 6; ++i) rr[i] = x[i];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = 0.0; }
+          for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = real(0.0); }
 #pragma unroll
           for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
         }
@@ -160,10 +190,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           if (i < nrec) ring[s][i][lane] = rr[i];
       }
       if (PIPE) __syncthreads();
+#ifdef MHPC_RO_TIMING
+      if (lane == 0 && w0 && run) {
+        const unsigned long long tk3 = clock64();
+        if (wb) {
+          ro_cyc[0] += tk1 - tk0; ro_cyc[1] += tk2 - tk1; ro_cyc[2] += tk3 - tk2; ro_cyc[4]++;
+        } else {
+          ro_cyc[3] += tk3 - tk0; ro_cyc[5]++;
+        }
+      }
+#endif
       if (w1 && run) {
-        double r[RING_W];
+        real r[RING_W];
 #pragma unroll
-        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[s][i][lane] : rr[i]) : 0.0;
+        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[s][i][lane] : rr[i]) : real(0.0);
         V += wb ? wb_running_cost(sp, mode, dt, refpos[k], r, r + 14, r + 18, reb, delta, etq, egr)
                 : fb_running_cost(sp, mode, dt, refpos[k], r, r + 6);
         store_rec(r, nrec, ko + k);
@@ -172,20 +212,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     // terminal state of the phase, then the transition (wave 0)
     const int s = PIPE ? (q & 1) : 0;
     ++q;
-    double xe[RING_W];
+    real xe[RING_W];
     if (w0 && run) {
 #pragma unroll
-      for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? x[i] : 0.0;
+      for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? x[i] : real(0.0);
       if (PIPE)
         for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
       if (wb && p + 1 < sp.P) {
         if (mode == 2 || mode == 4) {
-          double xp[14], lam[2];
-          wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+          real xp[14], lam[2];
+          wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
           for (int i = 0; i < 14; ++i) x[i] = xp[i];
         }
         if (p + 1 >= sp.n_wb) {
-          const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+          const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
           x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
         }
       }
@@ -195,30 +235,30 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       if (run) {
         if (PIPE) {
 #pragma unroll
-          for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? ring[s][i][lane] : 0.0;
+          for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? ring[s][i][lane] : real(0.0);
         }
-        double h = 0;
+        real h = 0;
         if (wb) {
-          double rx[14];
+          real rx[14];
           wb_term_ref(sp, mode, refpos[N - 1], rx);
-          double Phi = 0;
-          for (int i = 0; i < 14; ++i) { const double e = xe[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
-          Phi = Phi * 0.5;
+          real Phi = 0;
+          for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+          Phi = Phi * real(0.5);
           if (ntc_of(mode, true)) {
             h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
             if (sp.AL_active) {
-              const double sg = st->sigma[p], lam = st->lambda[p];
-              const double sh2 = sg * h / 2;
+              const real sg = st->sigma[p], lam = st->lambda[p];
+              const real sh2 = sg * h / 2;
               Phi += 50 * (sh2 * sh2 + lam * h);
             }
           }
           V += Phi;
         } else {
-          double rx[6];
+          real rx[6];
           fb_term_ref(sp, refpos[N - 1], rx);
-          double Phi = 0;
-          for (int i = 0; i < 6; ++i) { const double e = xe[i] - rx[i]; Phi += e * cQffb[i] * e; }
-          V += Phi * 0.5;
+          real Phi = 0;
+          for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQffb[i] * e; }
+          V += Phi * real(0.5);
         }
         J += V;
         viol2 += h * h;
@@ -233,6 +273,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     sViol[lane] = sqrt(viol2);
   }
   __syncthreads();
+#ifdef MHPC_RO_TIMING
+  if (lane == 0 && w0)
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_ro_cyc[i], ro_cyc[i]);
+#endif
   if (full) {
     if (w1 && run) {
       st->J = J;
@@ -253,11 +297,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     return;
   }
   if (w1 && run && j == 0) {
-    const double cost_prev = st->J;
+    const real cost_prev = st->J;
     int sel = nc - 1, nls = nc + 1;
     for (int c = 0; c < nc; ++c) {
-      const double e = sp.eps[c];
-      const double rhs = cost_prev + sp.gamma * e * (1 - e / 2) * st->dV_exp;
+      const real e = sp.eps[c];
+      const real rhs = cost_prev + sp.gamma * e * (1 - e / 2) * st->dV_exp;
       if (sJ[lane + c] <= rhs) { sel = c; nls = c + 1; break; }
     }
     const int sl = lane + sel;
@@ -296,96 +340,96 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 // C2 workload (256 concurrent rollouts of one nominal).  Lane = (problem, step size).
 // ============================================================================================
 __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, int n_eps,
-                                                    const double* eps_v, double* Jo,
-                                                    double* vo) {
+                                                    const real* eps_v, real* Jo,
+                                                    real* vo) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * n_eps) return;
   const int b = (int)(t / n_eps), e = (int)(t - (long)b * n_eps);
   const ProbState* st = &d.st[b];
   const int nom = st->nom_slot;
-  const double eps = eps_v[e];
+  const real eps = eps_v[e];
   const bool reb = st->reb_active != 0;
-  double x[14];
-  const double* x0 = d.x0 + (size_t)b * 14;
+  real x[14];
+  const real* x0 = d.x0 + (size_t)b * 14;
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
-  double J = 0, viol2 = 0;
+  real J = 0, viol2 = 0;
   for (int p = 0; p < sp.P; ++p) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const double dt = sp.dt[p];
-    const double* refpos = d.refpos + (size_t)b * sp.NK + ko;
-    double V = 0, h = 0;
+    const real dt = sp.dt[p];
+    const real* refpos = d.refpos + (size_t)b * sp.NK + ko;
+    real V = 0, h = 0;
     if (p < sp.n_wb) {
-      const double delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
+      const real delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
       for (int k = 0; k < N - 1; ++k) {
-        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
-        double u[4];
+        const real* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const real* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const real* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        real u[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          double fb = 0;
+          real fb = 0;
 #pragma unroll
           for (int c = 0; c < 14; ++c) fb += Kk[i * 14 + c] * (x[c] - nk[c]);
           u[i] = (nk[14 + i] + eps * duk[i]) + fb;
         }
-        double xd[14], y[4];
-        wb_dynamics<double>(x, u, mode, xd, y);
+        real xd[14], y[4];
+        wb_dynamics<real>(x, u, mode, xd, y);
         V += wb_running_cost(sp, mode, dt, refpos[k], x, u, y, reb, delta, etq, egr);
 #pragma unroll
         for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
       }
-      double rx[14];
+      real rx[14];
       wb_term_ref(sp, mode, refpos[N - 1], rx);
-      double Phi = 0;
-      for (int i = 0; i < 14; ++i) { const double ee = x[i] - rx[i]; Phi += ee * cQfwb[mode - 1][i] * ee; }
-      Phi = Phi * 0.5;
+      real Phi = 0;
+      for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * cQfwb[mode - 1][i] * ee; }
+      Phi = Phi * real(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
         if (sp.AL_active) {
-          const double sg = st->sigma[p], lam = st->lambda[p];
-          const double sh2 = sg * h / 2;
+          const real sg = st->sigma[p], lam = st->lambda[p];
+          const real sh2 = sg * h / 2;
           Phi += 50 * (sh2 * sh2 + lam * h);
         }
       }
       V += Phi;
       if (p + 1 < sp.P) {
         if (mode == 2 || mode == 4) {
-          double xp[14], lam[2];
-          wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+          real xp[14], lam[2];
+          wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
           for (int i = 0; i < 14; ++i) x[i] = xp[i];
         }
         if (p + 1 >= sp.n_wb) {
-          const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+          const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
           x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
         }
       }
     } else {
-      double f[4], sc[2];
+      real f[4], sc[2];
       plan_foothold(x, dt * N, mode, f);
       srb_contact(mode, sc);
       for (int k = 0; k < N - 1; ++k) {
-        const double* nk = traj_ptr(sp, d, b, nom, ko + k);
-        const double* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-        const double* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
-        double u[4];
+        const real* nk = traj_ptr(sp, d, b, nom, ko + k);
+        const real* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const real* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        real u[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          double fb = 0;
+          real fb = 0;
 #pragma unroll
           for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
           u[i] = (nk[6 + i] + eps * duk[i]) + fb;
         }
-        double xd[6];
+        real xd[6];
         srb_dynamics(x, u, f, sc, xd);
         V += fb_running_cost(sp, mode, dt, refpos[k], x, u);
 #pragma unroll
         for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
       }
-      double rx[6];
+      real rx[6];
       fb_term_ref(sp, refpos[N - 1], rx);
-      double Phi = 0;
-      for (int i = 0; i < 6; ++i) { const double ee = x[i] - rx[i]; Phi += ee * cQffb[i] * ee; }
-      V += Phi * 0.5;
+      real Phi = 0;
+      for (int i = 0; i < 6; ++i) { const real ee = x[i] - rx[i]; Phi += ee * cQffb[i] * ee; }
+      V += Phi * real(0.5);
     }
     J += V;
     viol2 += h * h;
@@ -402,7 +446,7 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
 // exact zeros (joint limits carry eps_ReB = 0; torque / GRF limits do not depend on x).
 // Lane = (problem, knot); lx [B][N-1][n], phix [B][n].
 // ============================================================================================
-__global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double* phix) {
+__global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* phix) {
   const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * N) return;
@@ -410,46 +454,46 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double
   const ProbState* st = &d.st[b];
   const bool wb = p < sp.n_wb;
   const int n = wb ? 14 : 6;
-  const double dt = sp.dt[p];
-  const double* x = traj_ptr(sp, d, b, st->par_slot, ko + k);
-  const double pos = d.refpos[(size_t)b * sp.NK + ko + k];
+  const real dt = sp.dt[p];
+  const real* x = traj_ptr(sp, d, b, st->par_slot, ko + k);
+  const real pos = d.refpos[(size_t)b * sp.NK + ko + k];
   if (k < N - 1) {
-    double* o = lx + ((size_t)b * (N - 1) + k) * n;
+    real* o = lx + ((size_t)b * (N - 1) + k) * n;
     for (int i = 0; i < n; ++i) {
-      double rxi, w2;
+      real rxi, w2;
       if (wb) {
-        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 2 ? 0.0
-              : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : 0.0;
+        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 2 ? real(0.0)
+              : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : real(0.0);
         w2 = 2 * dt * cQwb[i];
       } else {
-        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 3 ? sp.vel : 0.0;
+        rxi = i == 0 ? pos : i == 1 ? sp.height : i == 3 ? sp.vel : real(0.0);
         w2 = 2 * dt * cQfb[i];
       }
       o[i] = w2 * (x[i] - rxi);
     }
   } else {
-    double* o = phix + (size_t)b * n;
+    real* o = phix + (size_t)b * n;
     if (wb) {
-      double rx[14];
+      real rx[14];
       wb_term_ref(sp, mode, pos, rx);
       const bool al = ntc_of(mode, true) && st->par_al;
-      double h = 0, hx[14], Hs[3][3];
+      real h = 0, hx[14], Hs[3][3];
       if (al) {
         if (mode == 2) wb_touchdown_compact<kFront>(x, &h, hx, Hs);
         else wb_touchdown_compact<kBack>(x, &h, hx, Hs);
       }
-      const double s = st->par_sigma[p], lam = st->par_lambda[p];
-      double v[14];
+      const real s = st->par_sigma[p], lam = st->par_lambda[p];
+      real v[14];
       for (int i = 0; i < 14; ++i) {
         v[i] = cQfwb[mode - 1][i] * (x[i] - rx[i]);
         if (al) v[i] += 50 * (s * s / 2 * hx[i] * h + lam * hx[i]);
       }
       if (ntc_of(mode, true) && sp.AL_active) {  // trials of the last line search
-        const double s2 = st->ls_sigma[p], lam2 = st->ls_lambda[p];
+        const real s2 = st->ls_sigma[p], lam2 = st->ls_lambda[p];
         for (int j = 0; j < st->ls_nt; ++j) {
           const int slot = j < st->ls_nom ? j : j + 1;
-          const double* xt = traj_ptr(sp, d, b, slot, ko + k);
-          double ht, hxt[14], Hst[3][3];
+          const real* xt = traj_ptr(sp, d, b, slot, ko + k);
+          real ht, hxt[14], Hst[3][3];
           if (mode == 2) wb_touchdown_compact<kFront>(xt, &ht, hxt, Hst);
           else wb_touchdown_compact<kBack>(xt, &ht, hxt, Hst);
           for (int i = 0; i < 14; ++i) v[i] += 50 * (s2 * s2 / 2 * hxt[i] * ht + lam2 * hxt[i]);
@@ -457,7 +501,7 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double
       }
       for (int i = 0; i < 14; ++i) o[i] = v[i];
     } else {
-      double rx[6];
+      real rx[6];
       fb_term_ref(sp, pos, rx);
       for (int i = 0; i < 6; ++i) o[i] = cQffb[i] * (x[i] - rx[i]);
     }
@@ -473,15 +517,15 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, double* lx, double
 // ============================================================================================
 constexpr int SREC = KS + 56 + 4 + 14;
 
-__global__ void k_store_save(SolveParams sp, DevBufs d, double* store, int nbk) {
+__global__ void k_store_save(SolveParams sp, DevBufs d, real* store, int nbk) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * sp.NK) return;
   const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
   int p = 0;
   while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
   const int k = kk - sp.ko[p];
-  double* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
-  const double* r = traj_ptr(sp, d, b, d.st[b].nom_slot, kk);
+  real* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  const real* r = traj_ptr(sp, d, b, d.st[b].nom_slot, kk);
   for (int i = 0; i < KS; ++i) o[i] = r[i];
   const size_t rec = (size_t)b * sp.NK + kk;
   for (int i = 0; i < 56; ++i) o[KS + i] = d.K[rec * 56 + i];
@@ -489,19 +533,19 @@ __global__ void k_store_save(SolveParams sp, DevBufs d, double* store, int nbk) 
   for (int i = 0; i < 14; ++i) o[KS + 60 + i] = d.G[rec * 14 + i];
 }
 
-__global__ void k_store_load(SolveParams sp, DevBufs d, const double* store, int nbk) {
+__global__ void k_store_load(SolveParams sp, DevBufs d, const real* store, int nbk) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * sp.NK) return;
   const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
   int p = 0;
   while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
   const int k = kk - sp.ko[p];
-  const double* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
-  double* r = traj_ptr(sp, d, b, 0, kk);  // k_init(warm = 0) sets nom_slot = 0
+  const real* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  real* r = traj_ptr(sp, d, b, 0, kk);  // k_init(warm = 0) sets nom_slot = 0
   for (int i = 0; i < KS; ++i) r[i] = o[i];
   if (k == sp.N[p] - 1)  // u, y of the last knot are never rewritten by a sweep (B11): the
     for (int sl = 1; sl < sp.nslot; ++sl) {  // buffer's stale tail must follow any trial
-      double* q = traj_ptr(sp, d, b, sl, kk);
+      real* q = traj_ptr(sp, d, b, sl, kk);
       for (int i = 0; i < KS; ++i) q[i] = o[i];
     }
   const size_t rec = (size_t)b * sp.NK + kk;
@@ -510,7 +554,7 @@ __global__ void k_store_load(SolveParams sp, DevBufs d, const double* store, int
   for (int i = 0; i < 14; ++i) d.G[rec * 14 + i] = o[KS + 60 + i];
 }
 
-hipError_t launch_store(const SolveParams& sp, const DevBufs& d, double* store, int nbk, int save,
+hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, int nbk, int save,
                         hipStream_t s) {
   const long n = (long)sp.B * sp.NK;
   if (save)
@@ -554,27 +598,27 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
   if (VC || loc < (N - 1) * 7) {
     const int k = VC ? loc / 11 : loc / 7;
     const int dir = VC ? 7 + (loc - k * 11) : loc - k * 7;
-    const double* nk = traj_ptr(sp, d, b, nom, ko + k);
+    const real* nk = traj_ptr(sp, d, b, nom, ko + k);
     Dual u[4], f[14], y[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = Dual(nk[14 + i], 14 + i == dir ? 1.0 : 0.0);
+    for (int i = 0; i < 4; ++i) u[i] = Dual(nk[14 + i], 14 + i == dir ? real(1.0) : real(0.0));
     if (!VC) {
       Dual x[14];
 #pragma unroll
-      for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? 1.0 : 0.0);
+      for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
       wb_dynamics<Dual>(x, u, mode, f, y);
     } else {
-      double xq[7];
+      real xq[7];
       Dual xv[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         xq[i] = nk[i];
-        xv[i] = Dual(nk[7 + i], 7 + i == dir ? 1.0 : 0.0);
+        xv[i] = Dual(nk[7 + i], 7 + i == dir ? real(1.0) : real(0.0));
       }
-      wb_dynamics_qv<double, Dual>(xq, xv, u, mode, f, y);
+      wb_dynamics_qv<real, Dual>(xq, xv, u, mode, f, y);
     }
-    double* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-    double* out = rec + dir * 9;
+    real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+    real* out = rec + dir * 9;
 #pragma unroll
     for (int i = 0; i < 7; ++i) out[i] = f[7 + i].d;
     out[7] = mode == 1 ? y[2].d : y[0].d;
@@ -582,7 +626,7 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
     if (!VC && dir == 0) {
       // running-cost derivatives of controls and contact forces at the nominal knot
       // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
-      double c[14];
+      real c[14];
       wb_cost_uy_derivs(mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
                         st->eps_tq[p], st->eps_grf[p], c);
 #pragma unroll
@@ -590,12 +634,12 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
     }
   } else {
     const int dir = loc - (N - 1) * 7;
-    const double* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
+    const real* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
     Dual x[14], xp[14], lam[2];
 #pragma unroll
-    for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? 1.0 : 0.0);
+    for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
     wb_impact<Dual>(x, mode == 2 ? kFront : kBack, xp, lam);
-    double* out = d.px + ((size_t)b * MAXP + p) * 196 + dir * 14;
+    real* out = d.px + ((size_t)b * MAXP + p) * 196 + dir * 14;
 #pragma unroll
     for (int i = 0; i < 14; ++i) out[i] = xp[i].d;
   }
@@ -609,8 +653,8 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
   if (b >= sp.B) return;
   ProbState* st = &d.st[b];
   if (st->active) {
-    double up = st->cap_pen;  // _option.update_penalty = captured value, 0 if satisfied
-    if (st->viol < 0.03) up = 0;
+    real up = st->cap_pen;  // _option.update_penalty = captured value, 0 if satisfied
+    if (st->viol < real(0.03)) up = 0;
     st->opt_pen = up;
     for (int p = 0; p < sp.P; ++p) {
       const bool wb = p < sp.n_wb;
@@ -618,7 +662,7 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
       st->sigma[p] *= up;
       if (st->reb_active && wb) {
         st->delta[p] *= sp.update_relax;
-        if (st->delta[p] < 0.01) st->delta[p] = 0.01;
+        if (st->delta[p] < real(0.01)) st->delta[p] = real(0.01);
         st->eps_tq[p] *= sp.update_ReB;
         st->eps_grf[p] *= sp.update_ReB;
       }
@@ -637,8 +681,8 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
 __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= sp.B) return;
-  const double* x0 = d.x0 + (size_t)b * 14;
-  double* pos = d.refpos + (size_t)b * sp.NK;
+  const real* x0 = d.x0 + (size_t)b * 14;
+  real* pos = d.refpos + (size_t)b * sp.NK;
   for (int p = 0; p < sp.P; ++p) {
     const int ko = sp.ko[p];
     pos[ko] = p == 0 ? x0[0] : pos[sp.ko[p - 1] + sp.N[p - 1] - 1];
@@ -649,10 +693,10 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   for (int p = 0; p < MAXP; ++p) {
     st->V[p] = 0; st->dV[p] = 0; st->h[p] = 0; st->lambda[p] = 0;
     const bool wb = p < sp.n_wb && p < sp.P;
-    st->sigma[p] = (wb && ntc_of(sp.mode[p], true)) ? 5.0 : 0.0;
-    st->delta[p] = 0.1;
-    st->eps_tq[p] = 0.01;
-    st->eps_grf[p] = 0.01;
+    st->sigma[p] = (wb && ntc_of(sp.mode[p], true)) ? real(5.0) : real(0.0);
+    st->delta[p] = real(0.1);
+    st->eps_tq[p] = real(0.01);
+    st->eps_grf[p] = real(0.01);
   }
   st->status = MHPC_SOLVE_OK;
   // ReB flag as the options set it (what a sweep right after initialization() sees); the
@@ -674,45 +718,45 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   st->cap_reb = st->opt_reb;
   st->cap_pen = st->opt_pen;
   // warm start of the WB phases into slot 0 (bounding_PDcontrol, boundingPDControl.cpp:3-46)
-  double x[14];
+  real x[14];
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
-  const double qnom[4] = {PI / 4, -PI * 7 / 12, PI / 4, -PI * 7 / 12};
-  const double Kp[4] = {5 * 8.0, 5 * 1.0, 5 * 12.0, 5 * 10.0};
+  const real qnom[4] = {PI / 4, -PI * 7 / 12, PI / 4, -PI * 7 / 12};
+  const real Kp[4] = {5 * real(8.0), 5 * real(1.0), 5 * real(12.0), 5 * real(10.0)};
   for (int p = 0; p < sp.n_wb; ++p) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const double dt = sp.dt[p];
+    const real dt = sp.dt[p];
     for (int k = 0; k < N - 1; ++k) {
-      double u[4];
+      real u[4];
       if (mode == 1 || mode == 3) {
-        double J[14], Jd[14], v[2];
+        real J[14], Jd[14], v[2];
         if (mode == 1) { wb_foot_jacobian_f<kBack>(x, J, Jd); wb_leg_ext<kBack>(x, v); }
         else { wb_foot_jacobian_f<kFront>(x, J, Jd); wb_leg_ext<kFront>(x, v); }
-        const double sq = v[0] * v[0] + v[1] * v[1], nrm = sqrt(sq);
-        const double n0 = v[0] / nrm, n1 = v[1] / nrm;
-        const double F0 = -n0 * 2200.0 * (nrm - 0.2462), F1 = -n1 * 2200.0 * (nrm - 0.2462);
-        const double gain = mode == 1 ? 3 : 2.2;
+        const real sq = v[0] * v[0] + v[1] * v[1], nrm = sqrt(sq);
+        const real n0 = v[0] / nrm, n1 = v[1] / nrm;
+        const real F0 = -n0 * real(2200.0) * (nrm - real(0.2462)), F1 = -n1 * real(2200.0) * (nrm - real(0.2462));
+        const real gain = mode == 1 ? 3 : real(2.2);
         for (int i = 0; i < 4; ++i) u[i] = (J[3 + i] * F0 + J[7 + 3 + i] * F1) * gain;
       } else {
         for (int i = 0; i < 4; ++i) u[i] = Kp[i] * (qnom[i] - x[3 + i]) - x[10 + i];
       }
-      double xd[14], y[4];
-      wb_dynamics<double>(x, u, mode, xd, y);
-      double* o = traj_ptr(sp, d, b, 0, ko + k);
+      real xd[14], y[4];
+      wb_dynamics<real>(x, u, mode, xd, y);
+      real* o = traj_ptr(sp, d, b, 0, ko + k);
       for (int i = 0; i < 14; ++i) o[i] = x[i];
       for (int i = 0; i < 4; ++i) { o[14 + i] = u[i]; o[18 + i] = y[i]; }
       for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
     }
-    double* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
+    real* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
     for (int i = 0; i < 14; ++i) oe[i] = x[i];
     // phase transition exactly as the forward sweep does it (MultiPhaseDDP.cpp:351-379)
     if (p + 1 < sp.P) {
       if (mode == 2 || mode == 4) {
-        double xp[14], lam[2];
-        wb_impact<double>(x, mode == 2 ? kFront : kBack, xp, lam);
+        real xp[14], lam[2];
+        wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
         for (int i = 0; i < 14; ++i) x[i] = xp[i];
       }
       if (p + 1 >= sp.n_wb) {
-        const double t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+        const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
         x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
       }
     }
@@ -724,20 +768,20 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
     for (int i = 0; i < 6; ++i) x[i] = x0[i];
   for (int p = sp.n_wb; p < sp.P; ++p) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const double dt = sp.dt[p];
-    double f[4], s[2];
+    const real dt = sp.dt[p];
+    real f[4], s[2];
     plan_foothold(x, dt * N, mode, f);
     srb_contact(mode, s);
-    const double u[4] = {0.0, 0.0, 0.0, 0.0};
+    const real u[4] = {real(0.0), real(0.0), real(0.0), real(0.0)};
     for (int k = 0; k < N - 1; ++k) {
-      double xd[6];
+      real xd[6];
       srb_dynamics(x, u, f, s, xd);
-      double* o = traj_ptr(sp, d, b, 0, ko + k);
+      real* o = traj_ptr(sp, d, b, 0, ko + k);
       for (int i = 0; i < 6; ++i) o[i] = x[i];
-      for (int i = 0; i < 4; ++i) { o[6 + i] = u[i]; o[10 + i] = 0.0; }
+      for (int i = 0; i < 4; ++i) { o[6 + i] = u[i]; o[10 + i] = real(0.0); }
       for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
     }
-    double* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
+    real* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
     for (int i = 0; i < 6; ++i) oe[i] = x[i];
   }
 }
@@ -756,21 +800,21 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   ProbState* st = &d.st[b];
   if (!st->active) return;
   const int lane = threadIdx.x;
-  __shared__ double sc[MHPC_MAX_KNOTS];
-  __shared__ double sV[MAXP], sH[MAXP];
-  const bool reb_off = (st->viol > 0.05) || al_iter == 1;
+  __shared__ real sc[MHPC_MAX_KNOTS];
+  __shared__ real sV[MAXP], sH[MAXP];
+  const bool reb_off = (st->viol > real(0.05)) || al_iter == 1;
   // solve() captures _option.ReB_active at its start, restores it every AL iteration
   const int cap_reb = al_iter == 1 ? st->opt_reb : st->cap_reb;
   const bool reb = cap_reb && !reb_off;
   const int nom = st->nom_slot;
-  const double* refpos = d.refpos + (size_t)b * sp.NK;
+  const real* refpos = d.refpos + (size_t)b * sp.NK;
   for (int kk = lane; kk < sp.NK; kk += 64) {
     int p = 0;
     while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
     const int k = kk - sp.ko[p], mode = sp.mode[p];
-    double c = 0.0;
+    real c = real(0.0);
     if (k < sp.N[p] - 1) {
-      const double* r = traj_ptr(sp, d, b, nom, kk);
+      const real* r = traj_ptr(sp, d, b, nom, kk);
       if (p < sp.n_wb)
         c = wb_running_cost(sp, mode, sp.dt[p], refpos[kk], r, r + 14, r + 18, reb, st->delta[p],
                             st->eps_tq[p], st->eps_grf[p]);
@@ -782,37 +826,37 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   __syncthreads();
   if (lane < sp.P) {
     const int p = lane, mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    double V = 0, h = 0;
+    real V = 0, h = 0;
     for (int k = 0; k < N - 1; ++k) V += sc[ko + k];
-    const double* x = traj_ptr(sp, d, b, nom, ko + N - 1);
+    const real* x = traj_ptr(sp, d, b, nom, ko + N - 1);
     if (p < sp.n_wb) {
-      double rx[14];
+      real rx[14];
       wb_term_ref(sp, mode, refpos[ko + N - 1], rx);
-      double Phi = 0;
-      for (int i = 0; i < 14; ++i) { const double e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
-      Phi = Phi * 0.5;
+      real Phi = 0;
+      for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+      Phi = Phi * real(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
         if (sp.AL_active) {
-          const double s = st->sigma[p], lam = st->lambda[p];
-          const double sh2 = s * h / 2;
+          const real s = st->sigma[p], lam = st->lambda[p];
+          const real sh2 = s * h / 2;
           Phi += 50 * (sh2 * sh2 + lam * h);
         }
       }
       V += Phi;
     } else {
-      double rx[6];
+      real rx[6];
       fb_term_ref(sp, refpos[ko + N - 1], rx);
-      double Phi = 0;
-      for (int i = 0; i < 6; ++i) { const double e = x[i] - rx[i]; Phi += e * cQffb[i] * e; }
-      V += Phi * 0.5;
+      real Phi = 0;
+      for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; Phi += e * cQffb[i] * e; }
+      V += Phi * real(0.5);
     }
     sV[p] = V;
     sH[p] = h;
   }
   __syncthreads();
   if (lane == 0) {
-    double J = 0, viol2 = 0;
+    real J = 0, viol2 = 0;
     for (int p = 0; p < sp.P; ++p) {
       J += sV[p];
       viol2 += sH[p] * sH[p];
@@ -849,21 +893,21 @@ __global__ void k_export(SolveParams sp, DevBufs d) {
 }
 
 // ---- kernel-level parity hooks (batched CasADi replacements) -----------------------------
-__global__ void k_eval_wb_dyn(int n, int mode, const double* x, const double* u, double* xd,
-                              double* y) {
+__global__ void k_eval_wb_dyn(int n, int mode, const real* x, const real* u, real* xd,
+                              real* y) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  wb_dynamics<double>(x + (size_t)i * 14, u + (size_t)i * 4, mode, xd + (size_t)i * 14, y + (size_t)i * 4);
+  wb_dynamics<real>(x + (size_t)i * 14, u + (size_t)i * 4, mode, xd + (size_t)i * 14, y + (size_t)i * 4);
 }
 
-__global__ void k_eval_wb_par(int n, int mode, const double* x, const double* u, double* Ac,
-                              double* Bc, double* C, double* D) {
+__global__ void k_eval_wb_par(int n, int mode, const real* x, const real* u, real* Ac,
+                              real* Bc, real* C, real* D) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * 18) return;
   const int i = t / 18, dir = t % 18;
   Dual xx[14], uu[4], f[14], y[4];
-  for (int a = 0; a < 14; ++a) xx[a] = Dual(x[(size_t)i * 14 + a], a == dir ? 1.0 : 0.0);
-  for (int a = 0; a < 4; ++a) uu[a] = Dual(u[(size_t)i * 4 + a], 14 + a == dir ? 1.0 : 0.0);
+  for (int a = 0; a < 14; ++a) xx[a] = Dual(x[(size_t)i * 14 + a], a == dir ? real(1.0) : real(0.0));
+  for (int a = 0; a < 4; ++a) uu[a] = Dual(u[(size_t)i * 4 + a], 14 + a == dir ? real(1.0) : real(0.0));
   wb_dynamics<Dual>(xx, uu, mode, f, y);
   if (dir < 14) {
     for (int r = 0; r < 14; ++r) Ac[(size_t)i * 196 + r * 14 + dir] = f[r].d;
@@ -874,20 +918,20 @@ __global__ void k_eval_wb_par(int n, int mode, const double* x, const double* u,
   }
 }
 
-__global__ void k_eval_wb_impact(int n, int foot, const double* x, double* xp, double* Px) {
+__global__ void k_eval_wb_impact(int n, int foot, const real* x, real* xp, real* Px) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * 14) return;
   const int i = t / 14, dir = t % 14;
   Dual xx[14], yy[14], lam[2];
-  for (int a = 0; a < 14; ++a) xx[a] = Dual(x[(size_t)i * 14 + a], a == dir ? 1.0 : 0.0);
+  for (int a = 0; a < 14; ++a) xx[a] = Dual(x[(size_t)i * 14 + a], a == dir ? real(1.0) : real(0.0));
   wb_impact<Dual>(xx, foot, yy, lam);
   for (int r = 0; r < 14; ++r) Px[(size_t)i * 196 + r * 14 + dir] = yy[r].d;
   if (dir == 0)
     for (int r = 0; r < 14; ++r) xp[(size_t)i * 14 + r] = yy[r].v;
 }
 
-__global__ void k_eval_srb(int n, const double* x, const double* u, const double* p,
-                           const double* s, double* xd, double* Ac, double* Bc) {
+__global__ void k_eval_srb(int n, const real* x, const real* u, const real* p,
+                           const real* s, real* xd, real* Ac, real* Bc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   srb_dynamics(x + (size_t)i * 6, u + (size_t)i * 4, p + (size_t)i * 4, s + (size_t)i * 2, xd + (size_t)i * 6);
@@ -951,14 +995,14 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,
-                              const double* eps, double* J, double* viol, hipStream_t s) {
+                              const real* eps, real* J, real* viol, hipStream_t s) {
   const long n = (long)sp.B * n_eps;
   hipLaunchKernelGGL(k_eps_rollout, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, d, n_eps,
                      eps, J, viol);
   return hipGetLastError();
 }
-hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, double* lx,
-                            double* phix, hipStream_t s) {
+hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real* lx,
+                            real* phix, hipStream_t s) {
   const long n = (long)sp.B * sp.N[p];
   hipLaunchKernelGGL(k_cost_grad, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d, p, lx,
                      phix);
@@ -981,28 +1025,40 @@ hipError_t launch_export(const SolveParams& sp, const DevBufs& d, hipStream_t s)
   hipLaunchKernelGGL(k_export, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sp, d);
   return hipGetLastError();
 }
-hipError_t launch_eval_wb_dyn(int n, int mode, const double* x, const double* u, double* xd,
-                              double* y, hipStream_t s) {
+hipError_t launch_eval_wb_dyn(int n, int mode, const real* x, const real* u, real* xd,
+                              real* y, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_wb_dyn, dim3((n + 63) / 64), dim3(64), 0, s, n, mode, x, u, xd, y);
   return hipGetLastError();
 }
-hipError_t launch_eval_wb_par(int n, int mode, const double* x, const double* u, double* Ac,
-                              double* Bc, double* C, double* D, hipStream_t s) {
+hipError_t launch_eval_wb_par(int n, int mode, const real* x, const real* u, real* Ac,
+                              real* Bc, real* C, real* D, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_wb_par, dim3((n * 18 + 63) / 64), dim3(64), 0, s, n, mode, x, u, Ac,
                      Bc, C, D);
   return hipGetLastError();
 }
-hipError_t launch_eval_wb_impact(int n, int foot, const double* x, double* xp, double* Px,
+hipError_t launch_eval_wb_impact(int n, int foot, const real* x, real* xp, real* Px,
                                  hipStream_t s) {
   hipLaunchKernelGGL(k_eval_wb_impact, dim3((n * 14 + 63) / 64), dim3(64), 0, s, n, foot, x, xp, Px);
   return hipGetLastError();
 }
-hipError_t launch_eval_srb(int n, const double* x, const double* u, const double* p,
-                           const double* c, double* xd, double* Ac, double* Bc, hipStream_t s) {
+hipError_t launch_eval_srb(int n, const real* x, const real* u, const real* p,
+                           const real* c, real* xd, real* Ac, real* Bc, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_srb, dim3((n + 63) / 64), dim3(64), 0, s, n, x, u, p, c, xd, Ac, Bc);
   return hipGetLastError();
 }
 
-}  // namespace mhpc
+}  // namespace MHPC_NS
 
-
+#ifdef MHPC_RO_TIMING
+extern "C" int mhpc_dbg_ro_cycles(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_ro_cyc), sizeof(unsigned long long) * 6) !=
+      hipSuccess)
+    return 1;
+  if (reset) {
+    unsigned long long z[6] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_ro_cyc), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

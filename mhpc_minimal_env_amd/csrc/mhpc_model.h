@@ -19,35 +19,35 @@
 // factorisation of M (the reference's generated code uses an unpivoted QR instead; both agree
 // to ~1e-12, see tests/test_model_host.py).
 //
-// Everything is templated on the scalar so the same source runs in double (rollouts)
+// Everything is templated on the scalar so the same source runs in real (rollouts)
 // and in Dual (one Jacobian column per lane).
 #pragma once
 #include "mhpc_dual.h"
 
-namespace mhpc {
+namespace MHPC_NS {
 
 // ---- parameters baked into the reference's generated code ----------
-constexpr double kGrav = 9.81;
-constexpr double kBodyMass = 5.46;
-constexpr double kBodyInertia = 0.116419;        // about the body CoM
-constexpr double kHipX = 0.19;                   // hip joints at +-0.19 on the body axis
-constexpr double kThighMass = 1.268;
-constexpr double kThighCom = 0.02;               // CoM distance down the thigh
-constexpr double kThighInertiaJoint = 0.0047132; // about the hip joint
-constexpr double kThighLen = 0.209;              // hip -> knee
-constexpr double kShankMass = 0.128;
-constexpr double kShankCom = 0.061;
-constexpr double kShankInertiaJoint = 0.000972288;  // about the knee joint
-constexpr double kShankLen = 0.195;              // knee -> foot
-constexpr double kGroundHeight = -0.404;         // MHPCLocomotion.cpp:25, WB_FL*_terminal_constr.c
-constexpr double kThighInertiaCom = kThighInertiaJoint - kThighMass * kThighCom * kThighCom;
-constexpr double kShankInertiaCom = kShankInertiaJoint - kShankMass * kShankCom * kShankCom;
+constexpr real kGrav = real(9.81);
+constexpr real kBodyMass = real(5.46);
+constexpr real kBodyInertia = real(0.116419);        // about the body CoM
+constexpr real kHipX = real(0.19);                   // hip joints at +-0.19 on the body axis
+constexpr real kThighMass = real(1.268);
+constexpr real kThighCom = real(0.02);               // CoM distance down the thigh
+constexpr real kThighInertiaJoint = real(0.0047132); // about the hip joint
+constexpr real kThighLen = real(0.209);              // hip -> knee
+constexpr real kShankMass = real(0.128);
+constexpr real kShankCom = real(0.061);
+constexpr real kShankInertiaJoint = real(0.000972288);  // about the knee joint
+constexpr real kShankLen = real(0.195);              // knee -> foot
+constexpr real kGroundHeight = -real(0.404);         // MHPCLocomotion.cpp:25, WB_FL*_terminal_constr.c
+constexpr real kThighInertiaCom = kThighInertiaJoint - kThighMass * kThighCom * kThighCom;
+constexpr real kShankInertiaCom = kShankInertiaJoint - kShankMass * kShankCom * kShankCom;
 
 // SRB constants (FBDynamics.c:51-100): total mass and pitch inertia of the floating base.
-constexpr double kSrbMass = 8.2520000000000007;
-constexpr double kSrbInertia = 0.23216549759999999;
-constexpr double kSrbInvInertia = 4.3072722275163766;  // as folded by FBDynamics_par.c
-constexpr double kSrbInvMass = 1.2118274357731458e-01;
+constexpr real kSrbMass = real(8.2520000000000007);
+constexpr real kSrbInertia = real(0.23216549759999999);
+constexpr real kSrbInvInertia = real(4.3072722275163766);  // as folded by FBDynamics_par.c
+constexpr real kSrbInvMass = real(1.2118274357731458e-01);
 
 constexpr int kWbX = 14, kWbQ = 7, kWbU = 4, kWbY = 4;
 constexpr int kFbX = 6, kFbU = 4, kFbY = 4;
@@ -57,8 +57,8 @@ enum Foot { kFront = 0, kBack = 1 };
 // Two scalar types run through the model: Q for everything that depends on the
 // configuration q only (link sines/cosines, Jacobians, M and its factorisation) and V for
 // what also depends on qdot or u (link rates, bias h, Jdot qdot, accelerations, forces).
-// Q = V = double is the plain model; Q = V = Dual differentiates along a q direction; Q =
-// double, V = Dual differentiates along a qdot or u direction, where M, its factorisation
+// Q = V = real is the plain model; Q = V = Dual differentiates along a q direction; Q =
+// real, V = Dual differentiates along a qdot or u direction, where M, its factorisation
 // and the Jacobians carry exactly zero derivative -- the same numbers at a fraction of the
 // work (the Jacobian pass, k_partials).
 
@@ -96,15 +96,15 @@ MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g) {
 // The leg index is a template parameter everywhere so that no register array is indexed
 // with a run-time value (which would spill it to scratch memory on the GPU).
 template <class Q, class V, int F>
-MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, double l1, double l2, Q jx[5], Q jz[5], V* jdx,
+MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, real l1, real l2, Q jx[5], Q jz[5], V* jdx,
                            V* jdz) {
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   const LegGeo<Q, V>& L = g.leg[F];
   // d/da of l*(-sin a, -cos a) = l*(-cos a, sin a)
   const Q tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
   const Q tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
-  jx[0] = Q(1.0); jz[0] = Q(0.0);
-  jx[1] = Q(0.0); jz[1] = Q(1.0);
+  jx[0] = Q(real(1.0)); jz[0] = Q(real(0.0));
+  jx[1] = Q(real(0.0)); jz[1] = Q(real(1.0));
   jx[4] = tx2;    jz[4] = tz2;
   jx[3] = tx1 + tx2;
   jz[3] = tz1 + tz2;
@@ -120,7 +120,7 @@ MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // Contribution of the thigh and shank of leg F to M (packed) and h.  xv = qdot.
 template <class Q, class V, int F>
 MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
   const V thd2 = xv[2] * xv[2];
   const V hax = (-sg * kHipX) * g.cth * thd2;  // centripetal acceleration of the hip point
@@ -129,9 +129,9 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
   for (int b = 0; b < 2; ++b) {  // thigh, shank
     Q jx[5], jz[5];
     V jdx, jdz;
-    double m, ic;
+    real m, ic;
     if (b == 0) {
-      leg_point_jac<Q, V, F>(g, kThighCom, 0.0, jx, jz, &jdx, &jdz);
+      leg_point_jac<Q, V, F>(g, kThighCom, real(0.0), jx, jz, &jdx, &jdz);
       m = kThighMass; ic = kThighInertiaCom;
     } else {
       leg_point_jac<Q, V, F>(g, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
@@ -164,9 +164,9 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
 template <class Q, class V>
 MHPC_HD void wb_mass_bias(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
 #pragma unroll
-  for (int i = 0; i < 7; ++i) h[i] = V(0.0);
+  for (int i = 0; i < 7; ++i) h[i] = V(real(0.0));
 #pragma unroll
-  for (int i = 0; i < 28; ++i) M[i] = Q(0.0);
+  for (int i = 0; i < 28; ++i) M[i] = Q(real(0.0));
   M[tri(0, 0)] = Q(kBodyMass);
   M[tri(1, 1)] = Q(kBodyMass);
   M[tri(2, 2)] = Q(kBodyInertia);
@@ -195,7 +195,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
     const S a = M[tri(i0, i0)], b = M[tri(i1, i0)], c = M[tri(i1, i1)];
-    const S rdet = S(1.0) / (a * c - b * b);
+    const S rdet = S(real(1.0)) / (a * c - b * b);
     F.Li[l][0] = c * rdet;
     F.Li[l][1] = -b * rdet;
     F.Li[l][2] = a * rdet;
@@ -219,7 +219,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   const S c00 = s11 * s22 - s21 * s21;
   const S c10 = s21 * s20 - s10 * s22;
   const S c20 = s10 * s21 - s11 * s20;
-  const S rdet = S(1.0) / (s00 * c00 + s10 * c10 + s20 * c20);
+  const S rdet = S(real(1.0)) / (s00 * c00 + s10 * c10 + s20 * c20);
   F.Si[0] = c00 * rdet;
   F.Si[1] = c10 * rdet;
   F.Si[2] = (s00 * s22 - s20 * s20) * rdet;
@@ -261,13 +261,13 @@ MHPC_HD void wb_foot_jac_full(const V* xv, const WbGeo<Q, V>& g, Q J[2][7], V jd
   Q jx[5], jz[5];
   V jdx, jdz;
   leg_point_jac<Q, V, F>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   const V thd2 = xv[2] * xv[2];
   jd[0] = jdx + (-sg * kHipX) * g.cth * thd2;
   jd[1] = jdz + (sg * kHipX) * g.sth * thd2;
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
 #pragma unroll
-  for (int i = 0; i < 7; ++i) { J[0][i] = Q(0.0); J[1][i] = Q(0.0); }
+  for (int i = 0; i < 7; ++i) { J[0][i] = Q(real(0.0)); J[1][i] = Q(real(0.0)); }
 #pragma unroll
   for (int a = 0; a < 5; ++a) { J[0][idx[a]] = jx[a]; J[1][idx[a]] = jz[a]; }
 }
@@ -285,7 +285,7 @@ MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7]
     for (int i = 0; i < 7; ++i) Y[r][i] = J[r][i];
     arrow_solve<Q, Q>(M, F, Y[r]);
   }
-  Q A00 = Q(0.0), A01 = Q(0.0), A11 = Q(0.0);
+  Q A00 = Q(real(0.0)), A01 = Q(real(0.0)), A11 = Q(real(0.0));
   V r0 = -c[0], r1 = -c[1];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
@@ -295,7 +295,7 @@ MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7]
     r0 -= J[0][i] * v[i];
     r1 -= J[1][i] * v[i];
   }
-  const Q rdet = Q(1.0) / (A00 * A11 - A01 * A01);
+  const Q rdet = Q(real(1.0)) / (A00 * A11 - A01 * A01);
   lam[0] = (A11 * r0 - A01 * r1) * rdet;
   lam[1] = (A00 * r1 - A01 * r0) * rdet;
 #pragma unroll
@@ -333,7 +333,7 @@ MHPC_HD void wb_dynamics_qv(const Q* xq, const V* xv, const V* u, int mode, V* x
   for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
   arrow_solve<Q, V>(M, AF, v);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = V(0.0);
+  for (int i = 0; i < 4; ++i) y[i] = V(real(0.0));
   if (mode == 1) wb_stance<Q, V, kBack>(xv, g, M, AF, v, y);
   else if (mode == 3) wb_stance<Q, V, kFront>(xv, g, M, AF, v, y);
 #pragma unroll
@@ -364,8 +364,8 @@ MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
   S v[7], c[2];
 #pragma unroll
   for (int i = 0; i < 7; ++i) v[i] = x[7 + i];  // M^-1 (M qd-) = qd-
-  c[0] = S(0.0);
-  c[1] = S(0.0);
+  c[0] = S(real(0.0));
+  c[1] = S(real(0.0));
   kkt_contact<S, S>(M, AF, J, c, v, Lam);  // J qd+ = 0
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
@@ -384,48 +384,48 @@ MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
 // mode 4 / WB_FL2) with its gradient hx (14) and the 3x3 non-zero block of its Hessian on
 // the state indices (theta, hip, knee) of that leg.
 template <int F>
-MHPC_HD double wb_touchdown_value(const double* x) {
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
+MHPC_HD real wb_touchdown_value(const real* x) {
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
-  const double a1 = x[2] + x[ih];
-  const double a2 = a1 + x[ik];
+  const real a1 = x[2] + x[ih];
+  const real a2 = a1 + x[ik];
   return x[1] - sg * kHipX * sin(x[2]) - kThighLen * cos(a1) - kShankLen * cos(a2) - kGroundHeight;
 }
 
 template <int F>
-MHPC_HD void wb_touchdown_compact(const double* x, double* h, double* hx, double Hs[3][3]) {
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
+MHPC_HD void wb_touchdown_compact(const real* x, real* h, real* hx, real Hs[3][3]) {
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
-  double sth, cth, s1, c1, s2, c2;
+  real sth, cth, s1, c1, s2, c2;
   sin_cos(x[2], &sth, &cth);
-  const double a1 = x[2] + x[ih];
-  const double a2 = a1 + x[ik];
+  const real a1 = x[2] + x[ih];
+  const real a2 = a1 + x[ik];
   sin_cos(a1, &s1, &c1);
   sin_cos(a2, &s2, &c2);
   *h = x[1] - sg * kHipX * sth - kThighLen * c1 - kShankLen * c2 - kGroundHeight;
 #pragma unroll
-  for (int i = 0; i < 14; ++i) hx[i] = 0.0;
-  const double dk = kShankLen * s2;
-  const double dh = kThighLen * s1 + dk;
-  hx[1] = 1.0;
+  for (int i = 0; i < 14; ++i) hx[i] = real(0.0);
+  const real dk = kShankLen * s2;
+  const real dh = kThighLen * s1 + dk;
+  hx[1] = real(1.0);
   hx[2] = -sg * kHipX * cth + dh;
   hx[ih] = dh;
   hx[ik] = dk;
-  const double ek = kShankLen * c2;
-  const double eh = kThighLen * c1 + ek;
-  const double et = sg * kHipX * sth + eh;
+  const real ek = kShankLen * c2;
+  const real eh = kThighLen * c1 + ek;
+  const real et = sg * kHipX * sth + eh;
   Hs[0][0] = et; Hs[0][1] = eh; Hs[0][2] = ek;
   Hs[1][0] = eh; Hs[1][1] = eh; Hs[1][2] = ek;
   Hs[2][0] = ek; Hs[2][1] = ek; Hs[2][2] = ek;
 }
 
 // Dense form (row-major 14x14 Hessian) used by host checks and the eval hooks.
-MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double* hxx) {
-  double Hs[3][3];
+MHPC_HD void wb_touchdown(const real* x, int f, real* h, real* hx, real* hxx) {
+  real Hs[3][3];
   if (f == kFront) wb_touchdown_compact<kFront>(x, h, hx, Hs);
   else wb_touchdown_compact<kBack>(x, h, hx, Hs);
   const int id[3] = {2, 3 + 2 * f, 4 + 2 * f};
-  for (int i = 0; i < 196; ++i) hxx[i] = 0.0;
+  for (int i = 0; i < 196; ++i) hxx[i] = real(0.0);
   for (int a = 0; a < 3; ++a)
     for (int b = 0; b < 3; ++b) hxx[id[a] * 14 + id[b]] = Hs[a][b];
 }
@@ -433,23 +433,23 @@ MHPC_HD void wb_touchdown(const double* x, int f, double* h, double* hx, double*
 // Foot Jacobian J (2x7, row-major) and Jdot (2x7) as used by the PD warm start
 // (Jacob_F / Jacob_B; boundingPDControl.cpp:29,35).
 template <int F>
-MHPC_HD void wb_foot_jacobian_f(const double* x, double* J, double* Jd) {
-  WbGeo<double, double> g;
-  wb_geometry<double, double>(x, x + 7, g);
-  double Jm[2][7], jd[2];
-  wb_foot_jac_full<double, double, F>(x + 7, g, Jm, jd);
+MHPC_HD void wb_foot_jacobian_f(const real* x, real* J, real* Jd) {
+  WbGeo<real, real> g;
+  wb_geometry<real, real>(x, x + 7, g);
+  real Jm[2][7], jd[2];
+  wb_foot_jac_full<real, real, F>(x + 7, g, Jm, jd);
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
     for (int i = 0; i < 7; ++i) J[r * 7 + i] = Jm[r][i];
-  constexpr double sg = F == kFront ? 1.0 : -1.0;
-  const LegGeo<double, double>& L = g.leg[F];
-  const double thd = x[9];
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
+  const LegGeo<real, real>& L = g.leg[F];
+  const real thd = x[9];
 #pragma unroll
-  for (int i = 0; i < 14; ++i) Jd[i] = 0.0;
+  for (int i = 0; i < 14; ++i) Jd[i] = real(0.0);
   // d/dt of -l*cos a = l sin a * adot ; d/dt of l*sin a = l cos a * adot
-  const double kx = kShankLen * L.s2 * L.w2, kz = kShankLen * L.c2 * L.w2;
-  const double hx = kThighLen * L.s1 * L.w1 + kx, hz = kThighLen * L.c1 * L.w1 + kz;
+  const real kx = kShankLen * L.s2 * L.w2, kz = kShankLen * L.c2 * L.w2;
+  const real hx = kThighLen * L.s1 * L.w1 + kx, hz = kThighLen * L.c1 * L.w1 + kz;
   constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   Jd[0 * 7 + ik] = kx;  Jd[1 * 7 + ik] = kz;
   Jd[0 * 7 + ih] = hx;  Jd[1 * 7 + ih] = hz;
@@ -457,16 +457,16 @@ MHPC_HD void wb_foot_jacobian_f(const double* x, double* J, double* Jd) {
   Jd[1 * 7 + 2] = sg * kHipX * g.sth * thd + hz;
 }
 
-MHPC_HD void wb_foot_jacobian(const double* x, int f, double* J, double* Jd) {
+MHPC_HD void wb_foot_jacobian(const real* x, int f, real* J, real* Jd) {
   if (f == kFront) wb_foot_jacobian_f<kFront>(x, J, Jd);
   else wb_foot_jacobian_f<kBack>(x, J, Jd);
 }
 
 // Hip-to-foot vector of leg F (PlanarQuadruped::get_leg_ext_vec, PlanarQuadruped.cpp:195-205).
 template <int F>
-MHPC_HD void wb_leg_ext(const double* q, double* v) {
+MHPC_HD void wb_leg_ext(const real* q, real* v) {
   constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
-  double s1, c1, s2, c2;
+  real s1, c1, s2, c2;
   sin_cos(q[2] + q[ih], &s1, &c1);
   sin_cos(q[2] + q[ih] + q[ik], &s2, &c2);
   v[0] = -kThighLen * s1 - kShankLen * s2;
@@ -477,35 +477,35 @@ MHPC_HD void wb_leg_ext(const double* q, double* v) {
 // x = (px, pz, th, vx, vz, w), u = (FFx, FFz, FBx, FBz), p = footholds (pFx, pFz, pBx,
 // pBz), s = contact flags (front, back).  Operation order follows FBDynamics.c so the
 // SRB arithmetic is bit-identical to the reference's.
-MHPC_HD void srb_contact(int mode, double s[2]) {
-  s[0] = mode == 3 ? 1.0 : 0.0;
-  s[1] = mode == 1 ? 1.0 : 0.0;
+MHPC_HD void srb_contact(int mode, real s[2]) {
+  s[0] = mode == 3 ? real(1.0) : real(0.0);
+  s[1] = mode == 1 ? real(1.0) : real(0.0);
 }
 
-MHPC_HD void srb_dynamics(const double* x, const double* u, const double* p, const double* s,
-                          double* xd) {
+MHPC_HD void srb_dynamics(const real* x, const real* u, const real* p, const real* s,
+                          real* xd) {
   MHPC_NO_FMA
   xd[0] = x[3];
   xd[1] = x[4];
   xd[2] = x[5];
   xd[3] = (s[0] * u[0]) / kSrbMass + (s[1] * u[2]) / kSrbMass;
-  xd[4] = ((s[0] * u[1]) / kSrbMass + (s[1] * u[3]) / kSrbMass) + (-9.8100000000000005);
-  const double tf = ((p[1] - x[1]) * u[0] - (p[0] - x[0]) * u[1]) / kSrbInertia;
-  const double tb = ((p[3] - x[1]) * u[2] - (p[2] - x[0]) * u[3]) / kSrbInertia;
+  xd[4] = ((s[0] * u[1]) / kSrbMass + (s[1] * u[3]) / kSrbMass) + (-real(9.8100000000000005));
+  const real tf = ((p[1] - x[1]) * u[0] - (p[0] - x[0]) * u[1]) / kSrbInertia;
+  const real tb = ((p[3] - x[1]) * u[2] - (p[2] - x[0]) * u[3]) / kSrbInertia;
   xd[5] = s[0] * tf + s[1] * tb;
 }
 
 // Continuous Jacobians, dense row-major Ac (6x6) and Bc (6x4) (FBDynamics_par.c).
-MHPC_HD void srb_jacobians(const double* x, const double* u, const double* p, const double* s,
-                           double* Ac, double* Bc) {
+MHPC_HD void srb_jacobians(const real* x, const real* u, const real* p, const real* s,
+                           real* Ac, real* Bc) {
   MHPC_NO_FMA
-  for (int i = 0; i < 36; ++i) Ac[i] = 0.0;
-  for (int i = 0; i < 24; ++i) Bc[i] = 0.0;
+  for (int i = 0; i < 36; ++i) Ac[i] = real(0.0);
+  for (int i = 0; i < 24; ++i) Bc[i] = real(0.0);
   Ac[5 * 6 + 0] = s[0] * (kSrbInvInertia * u[1]) + s[1] * (kSrbInvInertia * u[3]);
   Ac[5 * 6 + 1] = -(s[0] * (kSrbInvInertia * u[0]) + s[1] * (kSrbInvInertia * u[2]));
-  Ac[0 * 6 + 3] = 1.0;
-  Ac[1 * 6 + 4] = 1.0;
-  Ac[2 * 6 + 5] = 1.0;
+  Ac[0 * 6 + 3] = real(1.0);
+  Ac[1 * 6 + 4] = real(1.0);
+  Ac[2 * 6 + 5] = real(1.0);
   Bc[3 * 4 + 0] = kSrbInvMass * s[0];
   Bc[5 * 4 + 0] = s[0] * (kSrbInvInertia * (p[1] - x[1]));
   Bc[4 * 4 + 1] = kSrbInvMass * s[0];
@@ -516,4 +516,4 @@ MHPC_HD void srb_jacobians(const double* x, const double* u, const double* p, co
   Bc[5 * 4 + 3] = -(s[1] * (kSrbInvInertia * (p[2] - x[0])));
 }
 
-}  // namespace mhpc
+}  // namespace MHPC_NS

@@ -19,9 +19,11 @@
 #pragma once
 #include <stdint.h>
 
+#include "mhpc_real.h"
+
 #include "../../include/mhpc_capi.h"
 
-namespace mhpc {
+namespace MHPC_NS {
 
 constexpr int KS = 24;        // doubles per knot record in traj
 constexpr int PS_JAC = 162;   // 18 tangent directions x (7 qddot + 2 contact-force rows)
@@ -42,13 +44,13 @@ enum {
 struct SolveParams {
   int B, P, n_wb, NK;
   int mode[MAXP], N[MAXP], ko[MAXP], xs[MAXP];
-  double dt[MAXP];
-  double vel, height;
+  real dt[MAXP];
+  real vel, height;
   int n_cand, nslot;
-  double eps[MAXC];          // line-search grid 1, alpha, alpha^2, ... (host libm)
-  double gamma, DDP_thresh, AL_thresh, update_penalty, update_relax, update_regularization,
+  real eps[MAXC];          // line-search grid 1, alpha, alpha^2, ... (host libm)
+  real gamma, DDP_thresh, AL_thresh, update_penalty, update_relax, update_regularization,
       update_ReB;
-  double eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
+  real eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
   int AL_active, ReB_active;
   int buf[MAXP];             // phase buffer of each phase (receding horizon, see k_store_*)
   // partials work items per problem and their prefix offsets per phase, in two classes:
@@ -58,9 +60,9 @@ struct SolveParams {
 };
 
 struct ProbState {
-  double J, viol, dV_exp, reg, cost_prev;
-  double V[MAXP], dV[MAXP], h[MAXP];
-  double sigma[MAXP], lambda[MAXP], delta[MAXP], eps_tq[MAXP], eps_grf[MAXP];
+  real J, viol, dV_exp, reg, cost_prev;
+  real V[MAXP], dV[MAXP], h[MAXP];
+  real sigma[MAXP], lambda[MAXP], delta[MAXP], eps_tq[MAXP], eps_grf[MAXP];
   int32_t status;      // mhpc_solve_status
   int32_t active;      // still inside the AL loop
   int32_t ddp_active;  // still inside the DDP loop of this AL iteration
@@ -76,32 +78,32 @@ struct ProbState {
   // forward_sweep_partials_only) for print_debugInfo's cost.txt: the nominal slot it saw,
   // whether the AL terms entered Phix (B1) and the sigma / lambda it used
   int32_t par_slot, par_al;
-  double par_sigma[MAXP], par_lambda[MAXP];
+  real par_sigma[MAXP], par_lambda[MAXP];
   // line-search trials run after that evaluation (only the final, converged line search of
   // an AL iteration): the reference's dynamics-only sweeps add their AL terms to Phix too
   // (guard quirk of SinglePhase.cpp:269), which cost.txt shows.  Trial j lives in slot
   // j < ls_nom ? j : j + 1.
   int32_t ls_nt, ls_nom;
-  double ls_sigma[MAXP], ls_lambda[MAXP];
+  real ls_sigma[MAXP], ls_lambda[MAXP];
   // MultiPhaseDDP::_option as solve() leaves it: ReB_active and update_penalty are rewritten
   // inside the AL loop (MultiPhaseDDP.cpp:178-183, 273-277) and the next solve() starts from
   // the rewritten values (captured at its first AL iteration: cap_*) -- visible across the
   // solves of a receding-horizon loop.  mhpc_initialize restores the handle's options.
   int32_t opt_reb, cap_reb;
-  double opt_pen, cap_pen;
+  real opt_pen, cap_pen;
 };
 
 struct DevBufs {
-  double* traj;
-  double* refpos;
-  double* K;
-  double* du;
-  double* G;
-  double* par;
-  double* px;
-  double* x0;
+  real* traj;
+  real* refpos;
+  real* K;
+  real* du;
+  real* G;
+  real* par;
+  real* px;
+  real* x0;
   ProbState* st;
-  double* out;    // export staging [B][NK][KS]
+  real* out;    // export staging [B][NK][KS]
 };
 
 // ---- cost weights (MHPCCost.cpp:24-75) and constraint constants (MHPCConstraints.cpp) --
@@ -112,7 +114,7 @@ struct DevBufs {
 #endif
 
 struct Weights {
-  double Q[4][14], R[4][4], S[4][4], Qf[4][14];
+  real Q[4][14], R[4][4], S[4][4], Qf[4][14];
 };
 
-}  // namespace mhpc
+}  // namespace MHPC_NS

@@ -1,5 +1,6 @@
 # Build alternate copies of libmhpc_amd.so with different compile-time tuning flags into
 # mhpc_minimal_env_amd/csrc/_build/var/<name>/ (travels with the gpurun snapshot).
+# (flags apply to the fp64 kernels; the fp32 objects and the dispatcher are the default build)
 # usage: bash tools/build_variants.sh name1 "-DFLAG=.." name2 "-DFLAG=.." ...
 set -e
 C=/root/repo/mhpc_minimal_env_amd/csrc
@@ -10,6 +11,7 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c -o $d/bws.o $C/mhpc_bws.hip &
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c -o $d/kern.o $C/mhpc_kernels.hip &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libmhpc_amd.so $d/bws.o $d/kern.o $C/_build/mhpc_runtime.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libmhpc_amd.so $d/bws.o $d/kern.o $C/_build/mhpc_runtime.o \
+      $C/_build/mhpc_kernels32.o $C/_build/mhpc_bws32.o $C/_build/mhpc_runtime32.o $C/_build/mhpc_capi.o
   echo "$name: $flags" > $d/FLAGS
 done

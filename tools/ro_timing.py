@@ -1,4 +1,4 @@
-"""Per-part cycle breakdown of the line-search rollout's WB knots (needs a -DMHPC_RO_TIMING
+"""Per-part cycle breakdown of the line-search rollout's knots (needs a -DMHPC_RO_TIMING
 build): python tools/ro_timing.py <lib.so> [batch]"""
 import ctypes
 import os
@@ -15,15 +15,16 @@ dbg.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 desc = configs.c3_desc()
 loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=B, device=0)
 loco.set_initial_condition(configs.x0_for(desc, B))
-buf = (ctypes.c_ulonglong * 5)()
+buf = (ctypes.c_ulonglong * 6)()
 for it in range(2):
     loco.initialization()
     dbg(buf, 1)
     loco.solve_mhpc()
     dbg(buf, 1)
 c = list(buf)
-n = c[4]
-print("batch", B, "WB knots timed (wave lane 0):", n)
-for name, v in zip(["feedback u", "wb_dynamics", "running cost", "store + step"], c[:4]):
+nw, nf = max(c[4], 1), max(c[5], 1)
+print("batch", B, "knots timed (lane 0 of each dynamics wave): WB", c[4], "SRB", c[5])
+for name, v, n in [("WB feedback u", c[0], nw), ("WB dynamics", c[1], nw),
+                   ("WB hand-over", c[2], nw), ("SRB knot", c[3], nf)]:
     print(f"{name:14s} {v / n:9.1f} cyc/knot")
-print(f"{'total':14s} {sum(c[:4]) / n:9.1f} cyc/knot")
+print(f"{'WB total':14s} {sum(c[:3]) / nw:9.1f} cyc/knot")
