@@ -36,7 +36,8 @@ template <int NX> struct QShape {
 };
 
 struct BwsLds {
-  real H[196], G[14];  // value function of knot k+1, then of knot k (row stride NX)
+  alignas(16) real H[196];
+  alignas(16) real G[14];  // value function of knot k+1, then of knot k (row stride NX)
   real W[7 * WS];      // rows NQ..NX-1 of [A B]
   real G2[2 * WS];     // stance rows of [C D]
   real l[JR];          // (lx, lu)
@@ -55,8 +56,10 @@ struct BwsLds {
   };
   real Qv[18];         // (Qx, Qu)
   real xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
-  real Kst[56], dust[4], Gst[14];     // results of the last knot, stored one knot later
+  alignas(16) real Kst[56];          // results of the last knot, stored one knot later
+  alignas(16) real dust[4];
   real hx[14], Hs[9], G2v[14];
+  real junk[64];       // write target of the spare lanes of a round (never read)
   real dV;
   int fail;
 #ifdef MHPC_BWS_TIMING
@@ -268,37 +271,44 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     static_assert(GR * T2 <= JR && GR * T2 <= QR && GR * T2 <= WS, "R2 padding");
     const int j = lane % NC, g = lane / NC;
     const bool isg = j == NX;
+    const bool wr = g < GR;                    // spare lanes write to the junk row
     const real* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
-    const int cs = isg ? 1 : NX;
     real hc[NQ];
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) hc[r] = col0[(NQ + r) * cs];
+    for (int r = 0; r < NQ; ++r) hc[r] = col0[isg ? NQ + r : (NQ + r) * NX];
+    real ly0 = real(0.0), ly1 = real(0.0);
+    if (HAS_Y) { ly0 = sh.ly2[0]; ly1 = sh.ly2[1]; }
+    // straight-line rows (no per-row branches, so the scheduler interleaves the T2 chains):
+    // the G-column extras are computed on every lane and selected
     constexpr int C = T2 < CH2 ? T2 : CH2;
-#pragma unroll 1
+#pragma unroll
     for (int t0 = 0; t0 < T2; t0 += C) {
       real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T2) continue;
         const int row = g + GR * (t0 + u);  // < JR
         const real a = coef_a<NQ>(row, dt);
-        const real hb = col0[coef_b<NQ>(row) * cs];
+        const int bi = coef_b<NQ>(row);
+        const real hb = col0[isg ? bi : bi * NX];
         real sacc = a != real(0.0) ? a * hb : real(0.0);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) sacc += sh.W[r * WS + row] * hc[r];
-        if (isg) {
-          real tt = real(0.0);
-          if (HAS_Y) tt = sh.G2[row] * sh.ly2[0] + sh.G2[WS + row] * sh.ly2[1];
-          sacc = (sh.l[row] + sacc) + tt;
-        }
-        acc[u] = sacc;
+        real tt = real(0.0);
+        if (HAS_Y) tt = sh.G2[row] * ly0 + sh.G2[WS + row] * ly1;
+        const real gs = (sh.l[row] + sacc) + tt;
+        acc[u] = isg ? gs : sacc;
       }
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T2) continue;
         const int row = g + GR * (t0 + u);
-        if (t0 + u < T2 && g < GR) *(isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * NX + j]) = acc[u];
+        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * NX + j];
+        *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
       }
     }
   }
+  BWS_TMARK(sh, lane, NQ == 3 ? 4 : 3);
   r2x();
   __syncthreads();
   BWS_TMARK(sh, lane, NQ == 3 ? 8 : 1);
@@ -309,6 +319,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     constexpr int RG = NT / NR, T3 = (NR + RG - 1) / RG;  // columns g + RG t < QV
     static_assert(RG * T3 <= QV && RG * T3 <= WS, "R3 padding");
     const int row = lane % NR, g = lane / NR;
+    const bool wr = g < RG;
     real jr[NQ];
 #pragma unroll
     for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
@@ -320,11 +331,12 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     }
     const real dg = sh.ldiag[row];
     constexpr int C = T3 < CH3 ? T3 : CH3;
-#pragma unroll 1
+#pragma unroll
     for (int t0 = 0; t0 < T3; t0 += C) {
       real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
         const real a = coef_a<NQ>(col, dt);
         const real jb = sh.Jt[row * NX + coef_b<NQ>(col)];
@@ -335,13 +347,14 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         real e2 = real(0.0);
         if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[WS + col];
         real v = (base + e2) + sacc;
-        if (row == col) v += real(1.0) * reg;
-        acc[u] = v;
+        const real vr = v + real(1.0) * reg;
+        acc[u] = row == col ? vr : v;
       }
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
-        if (t0 + u < T3 && g < RG) sh.Q[row * QS + col] = acc[u];
+        *(wr ? &sh.Q[row * QS + col] : &sh.junk[lane & 63]) = acc[u];
       }
     }
   }
@@ -432,11 +445,12 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int c = 0; c < 4; ++c) *(i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) = -tq[c];
     }
     constexpr int C = T5 < CH5 ? T5 : CH5;
-#pragma unroll 1
+#pragma unroll
     for (int t0 = 0; t0 < T5; t0 += C) {
       real acc[C];
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T5) continue;
         const int j = g + GC * (t0 + u);
         const int sj = j < NX ? j : QV;
         real sacc = 0;
@@ -449,12 +463,14 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       }
 #pragma unroll
       for (int u = 0; u < C; ++u) {
+        if (t0 + u >= T5) continue;
         const int j = g + GC * (t0 + u);
-        if (t0 + u < T5 && g < GC && i < NX && j <= NX)
-          *(j < NX ? &sh.H[i * NX + j] : &sh.G[i]) = acc[u];
+        const bool wr = g < GC && i < NX && j <= NX;
+        *(wr ? (j < NX ? &sh.H[i * NX + j] : &sh.G[i]) : &sh.junk[lane & 63]) = acc[u];
       }
     }
   }
+  BWS_TMARK(sh, lane, NQ == 3 ? 6 : 5);
   r45x();
   __syncthreads();
   BWS_TMARK(sh, lane, NQ == 3 ? 10 : 7);
@@ -640,6 +656,11 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
 // s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
 constexpr int kVmcnt0 = 0x0F70;
 
+#ifdef MHPC_FP32
+using real2 = float2;
+#else
+using real2 = double2;
+#endif
 // Store the staged K / du / G of knot record `rec`.  All global traffic of a knot (these
 // stores and the prefetch loads of the next record) is issued back to back right after the
 // wait for the previous prefetch, so the next wait (a full knot later) finds both retired:
@@ -650,12 +671,15 @@ __device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const B
 #ifdef MHPC_BWS_NOSTORE
   return;  // timing experiment only
 #endif
-#pragma unroll
-  for (int t = 0; t < (5 * NX + 4 + NT - 1) / NT; ++t) {
-    const int e = lane + NT * t;
-    if (e < 4 * NX) d.K[rec * 56 + e] = sh.Kst[e];
-    else if (e < 4 * NX + 4) d.du[rec * 4 + e - 4 * NX] = sh.dust[e - 4 * NX];
-    else if (e < 5 * NX + 4) d.G[rec * 14 + e - 4 * NX - 4] = sh.G[e - 4 * NX - 4];
+  // one 2-wide store per lane, one store instruction per knot: K (2 NX pairs), du (2), G
+  constexpr int NK2 = 2 * NX, NG2 = NX / 2;
+  static_assert(NK2 + 2 + NG2 <= NT, "flush lanes");
+  if (lane < NK2 + 2 + NG2) {
+    const bool isk = lane < NK2, isd = !isk && lane < NK2 + 2;
+    const int o = 2 * (isk ? lane : isd ? lane - NK2 : lane - NK2 - 2);
+    const real* src = isk ? sh.Kst : isd ? sh.dust : sh.G;
+    real* dst = isk ? d.K + rec * 56 : isd ? d.du + rec * 4 : d.G + rec * 14;
+    *reinterpret_cast<real2*>(dst + o) = *reinterpret_cast<const real2*>(src + o);
   }
 }
 

@@ -25,13 +25,14 @@ for it in range(2):
     dbg(buf, 1)
 c = loco.get_counters()
 cyc = np.array(list(buf), dtype=np.float64)
-names = ["total", "WB R2 (+stores/load)", "WB R3", "-", "-", "-", "-", "WB R45 (+drop)",
-         "SRB R2 (+stores/load)", "SRB R3", "SRB R45 (+drop)", ""]
+names = ["total", "WB R2 side (stores/load)", "WB R3", "WB R2 compute", "SRB R2 compute",
+         "WB R45 compute", "SRB R45 compute", "WB R45 side (drop)",
+         "SRB R2 side (stores/load)", "SRB R3", "SRB R45 side (drop)", ""]
 knots = c["bws_knots"]
 print("batch", B, "counters", c)
 print(f"{'round':24s} {'cyc/problem':>12s} {'cyc/knot':>10s} {'share':>7s}")
 # C3: half of the swept knots are WB, half SRB (per-kind cycles / (knots / 2))
-for i in [0, 1, 2, 7, 8, 9, 10]:
+for i in [0, 3, 1, 2, 5, 7, 4, 8, 9, 6, 10]:
     kn = knots if i == 0 else knots / 2
     print(f"{names[i]:24s} {cyc[i]/B:12.0f} {cyc[i]/kn:10.1f} {cyc[i]/cyc[0]:7.3f}")
 rest = cyc[0] - cyc[1:11].sum()
