@@ -43,11 +43,95 @@ using real2 = float2;
 using real2 = double2;
 #endif
 
+// native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
+typedef real sreal2 __attribute__((ext_vector_type(2)));
+constexpr int ST_PPW = 6;      // problems per staged wave (64 lanes / 10 candidates)
+constexpr int ST_PAIRS = 193;   // staged pairs per problem (192 + 1: problems on distinct LDS banks)
+constexpr int ST_RMAX = 128;    // staged position references per problem (knots per phase)
+
+// Line-search staging (ST): the 10 candidates of a problem share its nominal, gains and
+// references, so each wave loads them once per problem, cooperatively, one chunk of CH
+// knots ahead into registers (3 coalesced 2-wide loads per lane and problem) and drops
+// them into LDS at the next chunk boundary -- the serial knot chain then reads LDS instead
+// of waiting on a global-load round trip per knot (measured ~1.4k cycles per WB knot and
+// ~5k per SRB knot before, tools/ro_timing.py).  Per problem the stage holds 192 pairs:
+// [0, 128) the gain rows K (4 nx reals per knot), [128, ...) the nominal x, u (nx + 4
+// reals per knot) followed by du (4 reals per knot).  Load slots A / B (K) and C
+// (nominal + du) fill pairs [0, 64), [64, 128) and [128, 192) lane-linearly.
+template <bool WB>
+struct Stage {
+  static constexpr int NX = WB ? 14 : 6;
+  static constexpr int KP = 2 * NX;            // K pairs per knot: 28 / 12
+  static constexpr int TP = (NX + 4) / 2;      // nominal x,u pairs per knot: 9 / 5
+  static constexpr int CH = WB ? 4 : 8;        // knots per chunk
+  static constexpr int T0 = 128;               // first nominal pair
+  static constexpr int D0 = T0 + CH * TP;      // first du pair: 164 / 168
+  static_assert(CH * KP <= 128 && D0 + 2 * CH <= 192, "stage layout");
+};
+
+// Per-lane part of the stage addresses (reals from the problem's chunk base of each array)
+// and the chunk knot of each load slot; -1: the lane has no item in that slot.
+struct StageLane {
+  int offA, offB, offC, kcA, kcB, kcC;
+  bool trajC;
+};
+template <bool WB>
+__device__ __forceinline__ StageLane stage_lane(int lane) {
+  using S = Stage<WB>;
+  StageLane L;
+  const int pa = lane, pb = 64 + lane;
+  L.kcA = pa / S::KP; L.offA = L.kcA * 56 + 2 * (pa - L.kcA * S::KP);
+  L.kcB = pb / S::KP; L.offB = L.kcB * 56 + 2 * (pb - L.kcB * S::KP);
+  if (pb >= S::CH * S::KP) L.kcB = -1;
+  L.trajC = lane < S::CH * S::TP;
+  if (L.trajC) {
+    L.kcC = lane / S::TP; L.offC = L.kcC * KS + 2 * (lane - L.kcC * S::TP);
+  } else {
+    const int e = lane - S::CH * S::TP;
+    L.kcC = e < 2 * S::CH ? e / 2 : -1;
+    L.offC = 2 * e;
+  }
+  return L;
+}
+
+// Issue the loads of chunk [k0, k0 + CH) of phase (ko, nr rollout knots) into pf.  Every
+// load is unconditional (lanes without an item re-read the chunk base, absent problems
+// problem 0's): a masked load would merge with the register's old value and make the
+// compiler wait for it on the spot, which is exactly the round trip the stage hides.
+template <bool WB>
+__device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs& d,
+                                            const StageLane& L, int b0, int ko, int k0, int nr,
+                                            const int (&nomv)[ST_PPW], sreal2 (&pf)[ST_PPW * 3]) {
+  const int lim = nr - k0;  // chunk knots that exist
+  const int oA = L.kcA < lim ? L.offA : 0;
+  const int oB = L.kcB >= 0 && L.kcB < lim ? L.offB : 0;
+  const int oC = L.kcC >= 0 && L.kcC < lim ? L.offC : 0;
+#pragma unroll
+  for (int lp = 0; lp < ST_PPW; ++lp) {
+    const int nom = nomv[lp];  // < 0: problem absent or not iterating (uniform)
+    const int bb = nom >= 0 ? b0 + lp : 0;
+    const size_t kk = (size_t)bb * sp.NK + ko + k0;
+    const real* Kb = d.K + kk * 56;
+    const real* Tb = traj_ptr(sp, d, bb, nom >= 0 ? nom : 0, ko + k0);
+    const real* Db = d.du + kk * 4;
+    pf[3 * lp] = *reinterpret_cast<const sreal2*>(Kb + oA);
+    pf[3 * lp + 1] = *reinterpret_cast<const sreal2*>(Kb + oB);
+    pf[3 * lp + 2] = *reinterpret_cast<const sreal2*>((L.trajC ? Tb : Db) + oC);
+  }
+}
+
+// Drop a loaded chunk into the LDS stage (lane-linear per slot).
+__device__ __forceinline__ void stage_drop(int lane, const sreal2 (&pf)[ST_PPW * 3],
+                                           sreal2* stage2) {
+#pragma unroll
+  for (int i = 0; i < ST_PPW * 3; ++i) stage2[(i / 3) * ST_PAIRS + (i % 3) * 64 + lane] = pf[i];
+}
+
 // Optional cycle accounting of the rollout's knot loop (build with -DMHPC_RO_TIMING, read
 // with mhpc_dbg_ro_cycles; lane 0 of the dynamics wave of every block): 0 WB feedback u,
 // 1 WB dynamics, 2 WB record hand-over (ring + barrier), 3 SRB knot, 4 / 5 WB / SRB knots.
 #ifdef MHPC_RO_TIMING
-__device__ unsigned long long g_ro_cyc[6];
+__device__ unsigned long long g_ro_cyc[11];
 #define RO_T(v) const unsigned long long v = (lane == 0 && w0) ? clock64() : 0ull
 #define RO_ADD(i, v) do { if (lane == 0 && w0) ro_cyc[i] += (v); } while (0)
 #else
@@ -60,7 +144,9 @@ __device__ unsigned long long g_ro_cyc[6];
 // full = 1: forward_sweep(0) as a real rollout (one lane per problem, eps = 0, always
 // adopted) -- needed when the nominal is not a rollout of its own controls from x0, i.e.
 // after mhpc_update_problem (receding horizon); otherwise k_cost replaces it.
-template <bool PIPE>
+// ST = true: the line search reads nominal / gains / references through the LDS stage
+// (requires n_cand >= 10, i.e. <= ST_PPW problems per wave).
+template <bool PIPE, bool ST>
 __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, DevBufs d,
                                                              int al_iter, int ddp_iter,
                                                              int max_ddp, int full) {
@@ -75,11 +161,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   __shared__ real ring[PIPE ? 2 : 1][RING_W][64];
   __shared__ real sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
   __shared__ int sAny;
+  __shared__ int sNom[ST ? ST_PPW : 1];
+  __shared__ sreal2 stage2[ST ? ST_PPW * ST_PAIRS : 1];
+  __shared__ real sRef[ST ? ST_PPW : 1][ST ? ST_RMAX + 1 : 1];  // +1: distinct banks
 #ifdef MHPC_RO_TIMING
-  unsigned long long ro_cyc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long ro_cyc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
   if (t == 0) sAny = 0;
+  if (ST && t < ST_PPW) sNom[t] = -1;
   __syncthreads();
   bool run = false;
   int nom = 0, slot = 0;
@@ -91,7 +181,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     slot = j < nom ? j : j + 1;
   }
   if (w0 && run) sAny = 1;
+  if (ST && w0 && run && j == 0) sNom[lp] = nom;
   __syncthreads();
+  int nomv[ST_PPW];  // nominal slot of each staged problem, -1 if absent / not iterating
+#pragma unroll
+  for (int i = 0; i < ST_PPW; ++i) nomv[i] = ST ? __builtin_amdgcn_readfirstlane(sNom[i]) : -1;
   if (!sAny) return;  // uniform: no problem of this block is still iterating
   if (full && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
     if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
@@ -131,17 +225,51 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       srb_contact(mode, sc);
     }
     const real* refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
+    const int b0 = blockIdx.x * ppw;
+    // position references of the phase: staged in LDS by the cost wave (one round trip per
+    // phase), read from HBM per knot when the phase is longer than the stage
+    const bool sref = ST && N <= ST_RMAX;
+    if (sref && w1) {
+#pragma unroll
+      for (int i = 0; i < ST_PPW * ST_RMAX / 64; ++i) {
+        const int f = lane + 64 * i, rl = f / ST_RMAX, rk = f - rl * ST_RMAX;
+        if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
+      }
+    }
+    const real refT = (w1 && run) ? (sref ? sRef[lp][N - 1] : refpos[N - 1]) : real(0.0);
+    const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+    const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
+    const int D0 = wb ? Stage<true>::D0 : Stage<false>::D0;
+    const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
+    sreal2 pf[ST_PPW * 3];
+    if (ST && w0) {
+      if (wb) stage_issue<true>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
+      else stage_issue<false>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
+    }
     for (int k = 0; k < N - 1; ++k, ++q) {
       const int s = PIPE ? (q & 1) : 0;
       real rr[RING_W];
+      const int kc = k & (CH - 1);
       RO_T(tk0);
+      if (ST && w0 && kc == 0) {  // chunk boundary: drop the loaded chunk, fetch the next
+        stage_drop(lane, pf, stage2);
+#ifdef MHPC_RO_TIMING
+        if (lane == 0) { const unsigned long long tdr = clock64(); ro_cyc[10] += tdr - tk0; }
+#endif
+        if (k + CH < N - 1) {
+          if (wb) stage_issue<true>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
+          else stage_issue<false>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
+        }
+      }
 #ifdef MHPC_RO_TIMING
       unsigned long long tk1 = 0, tk2 = 0;
+      const unsigned long long tkc = (lane == 0 && w0) ? clock64() : 0ull;
 #endif
       if (w0 && run) {
-        const real* nk = traj_ptr(sp, d, b, nom, ko + k);
-        const real* Kk = d.K + ((size_t)b * sp.NK + ko + k) * 56;
-        const real* duk = d.du + ((size_t)b * sp.NK + ko + k) * 4;
+        const real* sgp = reinterpret_cast<const real*>(stage2 + lp * ST_PAIRS);
+        const real* nk = ST ? sgp + 2 * (Stage<true>::T0 + kc * TP) : traj_ptr(sp, d, b, nom, ko + k);
+        const real* Kk = ST ? sgp + 2 * kc * KP : d.K + ((size_t)b * sp.NK + ko + k) * 56;
+        const real* duk = ST ? sgp + 2 * (D0 + 2 * kc) : d.du + ((size_t)b * sp.NK + ko + k) * 4;
         if (wb) {
           real u[4];
 #pragma unroll
@@ -174,8 +302,14 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
             for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
             u[i] = (nk[6 + i] + eps * duk[i]) + fb;
           }
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk1 = clock64() + 0 * u[3];
+#endif
           real xd[6];
           srb_dynamics(x, u, f, sc, xd);
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk2 = clock64() + 0 * xd[5];
+#endif
 #pragma unroll
           for (int i = 0; i < 6; ++i) rr[i] = x[i];
 #pragma unroll
@@ -197,15 +331,18 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           ro_cyc[0] += tk1 - tk0; ro_cyc[1] += tk2 - tk1; ro_cyc[2] += tk3 - tk2; ro_cyc[4]++;
         } else {
           ro_cyc[3] += tk3 - tk0; ro_cyc[5]++;
+          ro_cyc[6] += tk1 - tk0; ro_cyc[7] += tk2 - tk1; ro_cyc[8] += tk3 - tk2;
         }
+        ro_cyc[9] += tkc - tk0;
       }
 #endif
       if (w1 && run) {
         real r[RING_W];
 #pragma unroll
         for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[s][i][lane] : rr[i]) : real(0.0);
-        V += wb ? wb_running_cost(sp, mode, dt, refpos[k], r, r + 14, r + 18, reb, delta, etq, egr)
-                : fb_running_cost(sp, mode, dt, refpos[k], r, r + 6);
+        const real pos = sref ? sRef[lp][k] : refpos[k];
+        V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, delta, etq, egr)
+                : fb_running_cost(sp, mode, dt, pos, r, r + 6);
         store_rec(r, nrec, ko + k);
       }
     }
@@ -240,7 +377,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         real h = 0;
         if (wb) {
           real rx[14];
-          wb_term_ref(sp, mode, refpos[N - 1], rx);
+          wb_term_ref(sp, mode, refT, rx);
           real Phi = 0;
           for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
           Phi = Phi * real(0.5);
@@ -255,7 +392,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           V += Phi;
         } else {
           real rx[6];
-          fb_term_ref(sp, refpos[N - 1], rx);
+          fb_term_ref(sp, refT, rx);
           real Phi = 0;
           for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQffb[i] * e; }
           V += Phi * real(0.5);
@@ -275,7 +412,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   __syncthreads();
 #ifdef MHPC_RO_TIMING
   if (lane == 0 && w0)
-    for (int i = 0; i < 6; ++i) atomicAdd(&g_ro_cyc[i], ro_cyc[i]);
+    for (int i = 0; i < 11; ++i) atomicAdd(&g_ro_cyc[i], ro_cyc[i]);
 #endif
   if (full) {
     if (w1 && run) {
@@ -967,8 +1104,8 @@ hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hip
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
                           int max_ddp, int full, hipStream_t s) {
   if (full) {
-    hipLaunchKernelGGL(k_rollout<false>, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, al_iter,
-                       0, 0, 1);
+    hipLaunchKernelGGL((k_rollout<false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d,
+                       al_iter, 0, 0, 1);
     return hipGetLastError();
   }
   const int ppw = 64 / sp.n_cand;
@@ -986,12 +1123,19 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   const bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
                                      // wave per block only competes for issue slots
 #endif
-  if (pipe)
-    hipLaunchKernelGGL(k_rollout<true>, dim3(nblk), dim3(128), 0, s, sp, d, al_iter, ddp_iter,
-                       max_ddp, 0);
+  const bool st = ppw <= ST_PPW;
+  if (pipe && st)
+    hipLaunchKernelGGL((k_rollout<true, true>), dim3(nblk), dim3(128), 0, s, sp, d, al_iter,
+                       ddp_iter, max_ddp, 0);
+  else if (pipe)
+    hipLaunchKernelGGL((k_rollout<true, false>), dim3(nblk), dim3(128), 0, s, sp, d, al_iter,
+                       ddp_iter, max_ddp, 0);
+  else if (st)
+    hipLaunchKernelGGL((k_rollout<false, true>), dim3(nblk), dim3(64), 0, s, sp, d, al_iter,
+                       ddp_iter, max_ddp, 0);
   else
-    hipLaunchKernelGGL(k_rollout<false>, dim3(nblk), dim3(64), 0, s, sp, d, al_iter, ddp_iter,
-                       max_ddp, 0);
+    hipLaunchKernelGGL((k_rollout<false, false>), dim3(nblk), dim3(64), 0, s, sp, d, al_iter,
+                       ddp_iter, max_ddp, 0);
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,
@@ -1052,11 +1196,11 @@ hipError_t launch_eval_srb(int n, const real* x, const real* u, const real* p,
 #ifdef MHPC_RO_TIMING
 extern "C" int mhpc_dbg_ro_cycles(unsigned long long* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_ro_cyc), sizeof(unsigned long long) * 6) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_ro_cyc), sizeof(unsigned long long) * 11) !=
       hipSuccess)
     return 1;
   if (reset) {
-    unsigned long long z[6] = {0};
+    unsigned long long z[11] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_ro_cyc), z, sizeof(z)) != hipSuccess) return 1;
   }
   return 0;

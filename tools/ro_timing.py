@@ -15,7 +15,7 @@ dbg.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 desc = configs.c3_desc()
 loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=B, device=0)
 loco.set_initial_condition(configs.x0_for(desc, B))
-buf = (ctypes.c_ulonglong * 6)()
+buf = (ctypes.c_ulonglong * 11)()
 for it in range(2):
     loco.initialization()
     dbg(buf, 1)
@@ -25,6 +25,8 @@ c = list(buf)
 nw, nf = max(c[4], 1), max(c[5], 1)
 print("batch", B, "knots timed (lane 0 of each dynamics wave): WB", c[4], "SRB", c[5])
 for name, v, n in [("WB feedback u", c[0], nw), ("WB dynamics", c[1], nw),
-                   ("WB hand-over", c[2], nw), ("SRB knot", c[3], nf)]:
+                   ("WB hand-over", c[2], nw), ("SRB knot", c[3], nf),
+                   ("SRB feedback u", c[6], nf), ("SRB dynamics", c[7], nf), ("SRB hand-over", c[8], nf),
+                   ("chunk stage", c[9], nw + nf), ("  of it: drop", c[10], nw + nf)]:
     print(f"{name:14s} {v / n:9.1f} cyc/knot")
 print(f"{'WB total':14s} {sum(c[:3]) / nw:9.1f} cyc/knot")
