@@ -420,7 +420,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
       s += t * sh.Q[(NX + c) * QS + QV];
     }
-    if (lane == 63 && psd) sh.dV += -s;
+    // s and psd are uniform: every lane writes the same value (no divergent branch)
+    const real dv0 = sh.dV;
+    sh.dV = psd ? dv0 + -s : dv0;
   }
   {
     // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
@@ -440,10 +442,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
       tq[c] = t;
     }
-    if (g == 0) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) *(i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) = -tq[c];
-    }
+    for (int c = 0; c < 4; ++c)
+      *(g == 0 ? (i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) : &sh.junk[lane & 63]) = -tq[c];
     constexpr int C = T5 < CH5 ? T5 : CH5;
 #pragma unroll
     for (int t0 = 0; t0 < T5; t0 += C) {
@@ -458,7 +459,8 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         for (int c = 0; c < 4; ++c) sacc += tq[c] * sh.Q[(NX + c) * QS + sj];
         const real qij = sh.Q[i * QS + sj];
         const real qji = sh.Q[(j < NX ? j : 0) * QS + i];
-        const real base = j < NX ? (qij + qji) / 2 : qij;
+        const real sym = (qij + qji) / 2;
+        const real base = j < NX ? sym : qij;
         acc[u] = base - sacc;
       }
 #pragma unroll
@@ -665,22 +667,36 @@ using real2 = double2;
 // stores and the prefetch loads of the next record) is issued back to back right after the
 // wait for the previous prefetch, so the next wait (a full knot later) finds both retired:
 // gfx950 keeps one in-order VM counter for loads and stores.
+// Per-lane part of flush_knot, fixed for a phase: one 2-wide store per lane, one store
+// instruction per knot: K (2 NX pairs), du (2), G (NX / 2).  Lanes past them repeat lane 0's
+// store (same address, same value), so the store needs no divergent branch.
+struct FlushLane {
+  real* base;   // d.K / d.du / d.G
+  int stride;   // reals per knot record of that array
+  int o;        // pair offset (reals) inside the record
+  int src;      // staged source in the LDS block (reals from its start)
+};
+template <int NX>
+__device__ __forceinline__ FlushLane flush_lane(const DevBufs& d, const BwsLds& sh, int lane) {
+  constexpr int NK2 = 2 * NX, NG2 = NX / 2;
+  const int l = lane < NK2 + 2 + NG2 ? lane : 0;
+  const bool isk = l < NK2, isd = !isk && l < NK2 + 2;
+  FlushLane f;
+  f.o = 2 * (isk ? l : isd ? l - NK2 : l - NK2 - 2);
+  f.base = isk ? d.K : isd ? d.du : d.G;
+  f.stride = isk ? 56 : isd ? 4 : 14;
+  const real* src = isk ? sh.Kst : isd ? sh.dust : sh.G;
+  f.src = (int)(src - reinterpret_cast<const real*>(&sh)) + f.o;
+  return f;
+}
 template <int NT, int NX>
-__device__ __forceinline__ void flush_knot(const DevBufs& d, size_t rec, const BwsLds& sh,
-                                           int lane) {
+__device__ __forceinline__ void flush_knot(size_t rec, const BwsLds& sh, const FlushLane& f) {
 #ifdef MHPC_BWS_NOSTORE
   return;  // timing experiment only
 #endif
-  // one 2-wide store per lane, one store instruction per knot: K (2 NX pairs), du (2), G
-  constexpr int NK2 = 2 * NX, NG2 = NX / 2;
-  static_assert(NK2 + 2 + NG2 <= NT, "flush lanes");
-  if (lane < NK2 + 2 + NG2) {
-    const bool isk = lane < NK2, isd = !isk && lane < NK2 + 2;
-    const int o = 2 * (isk ? lane : isd ? lane - NK2 : lane - NK2 - 2);
-    const real* src = isk ? sh.Kst : isd ? sh.dust : sh.G;
-    real* dst = isk ? d.K + rec * 56 : isd ? d.du + rec * 4 : d.G + rec * 14;
-    *reinterpret_cast<real2*>(dst + o) = *reinterpret_cast<const real2*>(src + o);
-  }
+  static_assert(2 * NX + 2 + NX / 2 <= NT, "flush lanes");
+  *reinterpret_cast<real2*>(f.base + rec * f.stride + f.o) =
+      *reinterpret_cast<const real2*>(reinterpret_cast<const real*>(&sh) + f.src);
 }
 
 // Backward sweep of one WB phase: knots N-2..0 with a one-knot register prefetch.
@@ -697,6 +713,10 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
   // prefetch registers: PT doubles of the partials record + 1 of the nominal knot
   constexpr int PT = (PS + NT - 1) / NT;
   real pre[PT], prex = 0;
+  real* const shf = reinterpret_cast<real*>(&sh);
+  const int junk = (int)(sh.junk - shf) + (lane & 63);
+  const int xo = lane < 22 ? lane : 0;
+  const bool isref = lane == 22;
   auto load = [&](int k) {
     const real* prec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
 #pragma unroll
@@ -705,43 +725,58 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
       pre[t] = prec[e < PS ? e : PS - 1];  // unconditional: no exec-masked load
     }
     const real* tk = traj_ptr(sp, d, b, nom, ko + k);
-    prex = *(lane < 22 ? tk + lane : lane == 22 ? pos + k : tk);
+    prex = *(isref ? pos + k : tk + xo);
   };
   const CostXConsts cx = wb_cost_x_consts(lane, sp, dt);
+  // Where each prefetched record element goes, fixed for the phase: value = pre * mul + base
+  // into the LDS block at dst (W entries: (I + dt Ac | dt Bc), everything else verbatim:
+  // x * 1 + (-0) == x exactly); elements with no target write the lane's junk slot.
+  int dst[PT];
+  real mul[PT], base[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int e = lane + NT * t;
+    dst[t] = junk;
+    mul[t] = real(1.0);
+    base[t] = -real(0.0);
+    if (e < PS_JAC) {
+      const int col = e / 9, r = e - col * 9;
+      if (r < 7) {
+        dst[t] = (int)(sh.W - shf) + r * WS + col;
+        mul[t] = dt;
+        base[t] = col == 7 + r ? real(1.0) : real(0.0);
+      } else if (stance) {
+        dst[t] = (int)(sh.G2 - shf) + (r - 7) * WS + col;
+      }
+    } else if (e < PS) {
+      const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
+      dst[t] = q < 4 ? (int)(sh.l - shf) + 14 + q
+             : q < 8 ? (int)(sh.ldiag - shf) + 14 + q - 4
+             : q < 10 ? (int)(sh.ly2 - shf) + q - 8 : (int)(sh.lyy2 - shf) + q - 10;
+    }
+  }
+  // lxx = 2 dt Q is constant over the phase (CostBase.cpp:28-31)
+  if (lane < 14) sh.ldiag[lane] = cx.w2;
+  const int dlx = lane < 14 ? (int)(sh.l - shf) + lane : junk;
   // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D],
-  // the control / force cost derivatives, and lx / lxx from the nominal state in prex
+  // the control / force cost derivatives, and lx from the nominal state in prex
   // (CostBase.cpp:28-31; lane 22 holds the position reference)
   auto drop = [&]() {
     __builtin_amdgcn_s_waitcnt(kVmcnt0);  // the prefetch (and the stores issued before it)
 #pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int e = lane + NT * t;
-      if (e < PS_JAC) {
-        const int col = e / 9, r = e - col * 9;
-        if (r < 7) sh.W[r * WS + col] = (col == 7 + r ? real(1.0) : real(0.0)) + pre[t] * dt;
-        else if (stance) sh.G2[(r - 7) * WS + col] = pre[t];
-      } else if (e < PS) {
-        const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
-        if (q < 4) sh.l[14 + q] = pre[t];
-        else if (q < 8) sh.ldiag[14 + q - 4] = pre[t];
-        else if (q < 10) sh.ly2[q - 8] = pre[t];
-        else sh.lyy2[q - 10] = pre[t];
-      }
-    }
+    for (int t = 0; t < PT; ++t) shf[dst[t]] = __builtin_fma(pre[t], mul[t], base[t]);
     const real pk = lane_bcast(prex, 22);
-    if (lane < 14) {
-      const real rxi = lane == 0 ? pk : cx.rx;
-      sh.l[lane] = cx.w2 * (prex - rxi);
-      sh.ldiag[lane] = cx.w2;
-    }
+    const real rxi = lane == 0 ? pk : cx.rx;
+    shf[dlx] = cx.w2 * (prex - rxi);
   };
+  const FlushLane fl = flush_lane<14>(d, sh, lane);
   load(N - 2);
   drop();
   __syncthreads();
   for (int k = N - 2; k >= 0; --k) {
     const int kk = ko + k;
     auto r2x = [&]() {
-      if (k < N - 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+      if (k < N - 2) flush_knot<NT, 14>((size_t)b * sp.NK + kk + 1, sh, fl);
       if (k > 0) load(k - 1);
     };
     auto r45x = [&]() {
@@ -751,7 +786,7 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     ++*knots;
     if (!ok) return false;
   }
-  if (N >= 2) flush_knot<NT, 14>(d, (size_t)b * sp.NK + ko, sh, lane);
+  if (N >= 2) flush_knot<NT, 14>((size_t)b * sp.NK + ko, sh, fl);
   return true;
 }
 
@@ -778,50 +813,62 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     fb_w2 = 2 * dt * cRfb[m][c];
     fb_rx = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
   }
+  const int xo = lane < 10 ? lane : 0;
+  const bool isref = lane == 10;
   auto loadx = [&](int k) {  // unconditional single load per lane (no exec-masked load)
     const real* tk = traj_ptr(sp, d, b, nom, ko + k);
-    return *(lane < 10 ? tk + lane : lane == 10 ? pos + k : tk);
+    return *(isref ? pos + k : tk + xo);
   };
+  real* const shf = reinterpret_cast<real*>(&sh);
+  const int junk = (int)(sh.junk - shf) + (lane & 63);
+  // cost derivative slot of the lane (lanes 30..35: lx of state i, 36..39: lu of control c)
+  const int dl = lane >= 30 && lane < 40 ? (int)(sh.l - shf) + lane - 30 : junk;
+  const int shsrc = lane >= 30 && lane < 40 ? lane - 30 : 0;
+  // lxx / luu = 2 dt Q / 2 dt R are constant over the phase
+  if (lane >= 30 && lane < 40) sh.ldiag[lane - 30] = fb_w2;
   // drop of knot k: the nominal (x 6, u 4) and position reference sit in prex of lanes
-  // 0..10; W rows (FBDynamics_par.c order) and the cost derivatives straight from registers
-  auto drop = [&](real px) {
+  // 0..10; W rows (FBDynamics_par.c order) and the cost derivatives straight from registers.
+  // Only six entries of W (row 5: the torque terms) depend on the knot: they are uniform,
+  // so every lane computes and writes them; the rest is written once per phase (full).
+  auto drop = [&](real px, bool full) {
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     const real xs[2] = {lane_bcast(px, 0), lane_bcast(px, 1)};
     const real us[4] = {lane_bcast(px, 6), lane_bcast(px, 7), lane_bcast(px, 8),
                           lane_bcast(px, 9)};
     const real pk = lane_bcast(px, 10);
-    const real own = __shfl(px, lane >= 36 ? lane - 30 : (lane >= 30 ? lane - 30 : 0));
-    if (lane < 30) {
-      const int r = lane / 10, col = lane - r * 10;
-      sh.W[r * WS + col] = srb_w_entry(r, col, xs, us, foot, cs, dt);
-    } else if (lane < 36) {
-      const int i = lane - 30;
-      const real rxi = i == 0 ? pk : fb_rx;
-      sh.l[i] = fb_w2 * (own - rxi);
-      sh.ldiag[i] = fb_w2;
-    } else if (lane < 40) {
-      const int c = lane - 36;
-      sh.l[6 + c] = fb_w2 * (own - fb_rx);
-      sh.ldiag[6 + c] = fb_w2;
+    const real own = __shfl(px, shsrc);
+    if (full) {
+      if (lane < 30) {
+        const int r = lane / 10, col = lane - r * 10;
+        sh.W[r * WS + col] = srb_w_entry(r, col, xs, us, foot, cs, dt);
+      }
+    } else {
+      sh.W[2 * WS + 0] = srb_w_entry(2, 0, xs, us, foot, cs, dt);
+      sh.W[2 * WS + 1] = srb_w_entry(2, 1, xs, us, foot, cs, dt);
+#pragma unroll
+      for (int c = 6; c < 10; ++c) sh.W[2 * WS + c] = srb_w_entry(2, c, xs, us, foot, cs, dt);
     }
+    const real rxi = lane == 30 ? pk : fb_rx;
+    shf[dl] = fb_w2 * (own - rxi);
   };
+  const FlushLane fl = flush_lane<6>(d, sh, lane);
   real prex = loadx(N - 2);
-  drop(prex);
+  drop(prex, true);
   __syncthreads();
   for (int k = N - 2; k >= 0; --k) {
     const int kk = ko + k;
     auto r2x = [&]() {
-      if (k < N - 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + kk + 1, sh, lane);
+      if (k < N - 2) flush_knot<NT, 6>((size_t)b * sp.NK + kk + 1, sh, fl);
       if (k > 0) prex = loadx(k - 1);
     };
     auto r45x = [&]() {
-      if (k > 0) drop(prex);
+      if (k > 0) drop(prex, false);
     };
     const bool ok = riccati_knot<NT, 3, false>(sh, lane, dt, reg, sp.eps9, r2x, r45x);
     ++*knots;
     if (!ok) return false;
   }
-  if (N >= 2) flush_knot<NT, 6>(d, (size_t)b * sp.NK + ko, sh, lane);
+  if (N >= 2) flush_knot<NT, 6>((size_t)b * sp.NK + ko, sh, fl);
   return true;
 }
 
