@@ -49,6 +49,37 @@ static __device__ __forceinline__ real* traj_ptr(const SolveParams& sp, const De
 
 static __device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (mode == 2 || mode == 4); }
 
+// Natural log of a positive argument (the barrier's g > delta > 0 and delta itself).  fp64:
+// the fdlibm algorithm (e_log.c: x = 2^k (1 + f) with sqrt(2)/2 <= 1 + f < sqrt(2),
+// s = f / (2 + f), a degree-14 odd polynomial in s), < 1 ulp -- about a third of the
+// instructions of the library log, whose extra work covers denormal scaling and special
+// values this path never sees.  The line search evaluates up to 11 of these per WB knot
+// and candidate while the ReB barrier is active.
+static __device__ __forceinline__ real log_pos(real x) {
+#ifdef MHPC_FP32
+  return logf(x);
+#else
+  int k;
+  double m = frexp(x, &k);  // x = m 2^k, m in [0.5, 1)
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 +
+                                                         w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 +
+                              w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * 6.93147180369123816490e-01 -
+         ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+#endif
+}
+
 // ---- reduced barrier (SinglePhase.cpp:298-317), k = 2 ---------------------------------
 // The reference's pow() calls with integer exponents are evaluated exactly as products:
 // pow(t, 2) = t*t (the correctly rounded square), pow(t, 1) = t, pow(t, 0) = 1 (also for
@@ -56,12 +87,12 @@ static __device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (
 static __device__ __forceinline__ void reduced_barrier(real g, real delta, real* B, real* Bz,
                                                 real* Bzz) {
   if (g > delta) {
-    *B = -log(g);
+    *B = -log_pos(g);
     *Bz = -1.0 / g;
     *Bzz = 1.0 / (g * g);
   } else {
     const real t = (g - 2 * delta) / ((2 - 1) * delta);
-    *B = (real)(2 - 1) / 2 * (t * t - 1) - log(delta);
+    *B = (real)(2 - 1) / 2 * (t * t - 1) - log_pos(delta);
     *Bz = t / delta;
     *Bzz = 1.0;
   }
