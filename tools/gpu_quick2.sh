@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/tests.log; exit 1; }
 tail -1 gpurun_out/tests.log
 for b in ${BATCHES:-1024 4096}; do
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --batch-per-gpu $b --no-cpu-baseline > gpurun_out/bench_b$b.json 2> gpurun_out/bench.err || { echo "BENCH FAILED"; tail gpurun_out/bench.err; exit 1; }
+  timeout -k 10 300 python bench.py --steps ${STEPS:-6} --warmup 2 --batch-per-gpu $b --no-cpu-baseline > gpurun_out/bench_b$b.json 2> gpurun_out/bench.err || { echo "BENCH FAILED"; tail gpurun_out/bench.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/bench_b$b.json')); print($b, round(d['value']), {k: round(v, 2) for k, v in d['kernel_ms_per_step'].items()})"
 done
 V=mhpc_minimal_env_amd/csrc/_build/var
