@@ -247,7 +247,7 @@ __device__ __forceinline__ int coef_b(int col) {
 #define MHPC_BWS_CH2 3
 #endif
 #ifndef MHPC_BWS_CH3
-#define MHPC_BWS_CH3 3
+#define MHPC_BWS_CH3 2
 #endif
 #ifndef MHPC_BWS_CH5
 #define MHPC_BWS_CH5 4
