@@ -732,9 +732,13 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
   const int loc = it - off[p];
   const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
   const int nom = st->nom_slot;
-  if (VC || loc < (N - 1) * 7) {
-    const int k = VC ? loc / 11 : loc / 7;
-    const int dir = VC ? 7 + (loc - k * 11) : loc - k * 7;
+  // The planar model is invariant to the base position (x, z) and its velocity (xdot,
+  // zdot): the columns of directions 0, 1, 7, 8 are exact zeros (the reference's CasADi
+  // Jacobians carry them as structural zeros), written once when the buffer is created, so
+  // only 5 configuration and 9 velocity / control directions per knot get a lane.
+  if (VC || loc < (N - 1) * PAR_QD) {
+    const int k = VC ? loc / PAR_VD : loc / PAR_QD;
+    const int dir = VC ? 9 + (loc - k * PAR_VD) : 2 + (loc - k * PAR_QD);
     const real* nk = traj_ptr(sp, d, b, nom, ko + k);
     Dual u[4], f[14], y[4];
 #pragma unroll
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
     for (int i = 0; i < 7; ++i) out[i] = f[7 + i].d;
     out[7] = mode == 1 ? y[2].d : y[0].d;
     out[8] = mode == 1 ? y[3].d : y[1].d;
-    if (!VC && dir == 0) {
+    if (!VC && dir == 2) {
       // running-cost derivatives of controls and contact forces at the nominal knot
       // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
       real c[14];
@@ -770,7 +774,7 @@ __global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_
       for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
     }
   } else {
-    const int dir = loc - (N - 1) * 7;
+    const int dir = loc - (N - 1) * PAR_QD;
     const real* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
     Dual x[14], xp[14], lam[2];
 #pragma unroll

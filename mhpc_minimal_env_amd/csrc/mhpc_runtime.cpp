@@ -112,8 +112,8 @@ static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
     sp.par_item_off[p] = items;
     sp.par_v_off[p] = items_v;
     if (wb) {
-      items += (desc.N[p] - 1) * 7 + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
-      items_v += (desc.N[p] - 1) * 11;
+      items += (desc.N[p] - 1) * PAR_QD + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
+      items_v += (desc.N[p] - 1) * PAR_VD;
     }
   }
   for (int p = sp.P; p <= MAXP; ++p) {
@@ -266,6 +266,8 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   // zero x0 on the handle's own (non-blocking) stream: a null-stream memset would not be
   // ordered before mhpc_set_x0's copy on this stream
   if (e == hipSuccess) e = hipMemsetAsync(d.x0, 0, B * 14 * sizeof(real), h->stream);
+  // the zero Jacobian columns of the partials records are never written by a kernel
+  if (e == hipSuccess) e = hipMemsetAsync(d.par, 0, B * NK * PS * sizeof(real), h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   byte_model(h);
   if (e != hipSuccess) {
@@ -631,6 +633,7 @@ int api_update_problem(Handle* h, const mhpc_gait* gait) {
       HIPCHK(hipMalloc((void**)arr[i], B * NK * per[i] * sizeof(real)));
     }
     HIPCHK(hipMemsetAsync(d.traj, 0, B * sp.nslot * NK * KS * sizeof(real), h->stream));
+    HIPCHK(hipMemsetAsync(d.par, 0, B * NK * PS * sizeof(real), h->stream));
     h->nk_cap = sp.NK;
   }
   h->sp = sp;

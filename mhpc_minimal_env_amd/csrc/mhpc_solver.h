@@ -29,6 +29,8 @@ constexpr int KS = 24;        // doubles per knot record in traj
 constexpr int PS_JAC = 162;   // 18 tangent directions x (7 qddot + 2 contact-force rows)
 constexpr int PS = 176;       // doubles per knot in par: Jacobians + 14 cost derivatives
                               // (lu 4, luu 4, ly 2, lyy 4 of the stance block)
+constexpr int PAR_QD = 5;      // partials lanes per WB knot: configuration directions 2..6
+constexpr int PAR_VD = 9;      // velocity / control directions 9..17 (0, 1, 7, 8: exact zeros)
 constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
 constexpr int TRACE = MHPC_TRACE_LEN;
