@@ -1092,6 +1092,28 @@ hipError_t launch_reduce_counters(const SolveParams& sp, const DevBufs& d,
   hipLaunchKernelGGL(k_reduce_counters, dim3((sp.B + 255) / 256), dim3(256), 0, s, sp, d, out);
   return hipGetLastError();
 }
+// memory_reset's zeros where a solve reads them before writing: u and y of every phase's
+// last knot in every trajectory slot (no rollout writes them, quirk B11; a slot becoming the
+// nominal carries them into the exports).  Everything else of traj is written before it is
+// read (slot 0 by k_init, the candidate slots by the line search), so initialize does not
+// clear the whole array (2.8 GB at batch 4096).
+__global__ void k_zero_tails(SolveParams sp, DevBufs d) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)sp.B * sp.nslot * sp.P;
+  if (t >= n) return;
+  const int p = (int)(t % sp.P);
+  const long bs = t / sp.P;
+  const int slot = (int)(bs % sp.nslot), b = (int)(bs / sp.nslot);
+  const int nx = p < sp.n_wb ? 14 : 6;
+  real* r = traj_ptr(sp, d, b, slot, sp.ko[p] + sp.N[p] - 1);
+  for (int i = nx; i < KS; ++i) r[i] = real(0.0);
+}
+hipError_t launch_zero_tails(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
+  const long n = (long)sp.B * sp.nslot * sp.P;
+  hipLaunchKernelGGL(k_zero_tails, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sp, d);
+  return hipGetLastError();
+}
+
 hipError_t launch_reset(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
   hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
   return hipGetLastError();

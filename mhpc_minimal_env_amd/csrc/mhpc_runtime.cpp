@@ -19,6 +19,7 @@ hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, hipStream_t);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_zero_tails(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, hipStream_t);
 // N_TIMESTEPS_MAX (MHPCLocomotion.h): knots per phase buffer; record = x,u,y + K + du + G
 constexpr int kPhaseBufKnots = 110;
@@ -344,7 +345,7 @@ static int initialize_async(Handle* h) {
   const SolveParams& sp = h->sp;
   DevBufs& d = h->d;
   const size_t B = sp.B, NK = sp.NK;
-  HIPCHK(hipMemsetAsync(d.traj, 0, B * sp.nslot * NK * KS * sizeof(real), h->stream));
+  HIPCHK(launch_zero_tails(sp, d, h->stream));
   HIPCHK(hipMemsetAsync(d.K, 0, B * NK * 56 * sizeof(real), h->stream));
   HIPCHK(hipMemsetAsync(d.du, 0, B * NK * 4 * sizeof(real), h->stream));
   HIPCHK(hipMemsetAsync(d.G, 0, B * NK * 14 * sizeof(real), h->stream));
