@@ -1,0 +1,22 @@
+# Round evidence in one GPU call: parity tests + smoke, C3 bench lines (batch 1024 with the
+# CPU baseline, 4096), C2 / C5 / C5-fp32 bench lines, rocprofv3 kernel stats + PMC HBM
+# traffic at batch 1024 and 4096.  usage: bash tools/gpu_evidence.sh <tag>
+set -o pipefail
+TAG=${1:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests_${TAG}.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/tests_${TAG}.log; exit 1; }
+tail -1 gpurun_out/tests_${TAG}.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 || { echo "SMOKE FAILED"; tail -20 gpurun_out/smoke_${TAG}.log; exit 1; }
+tail -1 gpurun_out/smoke_${TAG}.log
+run() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_${TAG}_$n.json 2> gpurun_out/bench_${TAG}_$n.err || { echo "bench $n failed"; tail gpurun_out/bench_${TAG}_$n.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_$n.json'));print('$n', round(d['value']), d['unit'], round(d['ms_per_step'],3), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"
+}
+run b1024
+run b4096 --batch-per-gpu 4096 --no-cpu-baseline
+run c2_b1 --workload c2
+run c2_b1024 --workload c2 --batch-per-gpu 1024 --no-cpu-baseline
+run c5_b4096 --workload c5 --cpu-sample 2048
+run c5f32_b4096 --workload c5f32 --no-cpu-baseline
+bash tools/gpu_profile.sh ${TAG}_b1024 1024 && bash tools/gpu_profile.sh ${TAG}_b4096 4096
