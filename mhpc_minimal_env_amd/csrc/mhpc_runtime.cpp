@@ -146,7 +146,8 @@ static void byte_model(Handle* h) {
     if (!wb) ib += N * kB * 14;
     if (wb) {
       const bool imp = sp.mode[p] == 2 || sp.mode[p] == 4;
-      pb += (N - 1) * kB * (18 + PS) + (imp ? kB * (14 + 196) : 0.0);
+      // x,u read; the record written without its four zero columns (written once at create)
+      pb += (N - 1) * kB * (18 + PS - 4 * 9) + (imp ? kB * (14 + 196) : 0.0);
       ib += N * kB * 22;
     }
   }
