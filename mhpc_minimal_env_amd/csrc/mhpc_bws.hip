@@ -57,6 +57,7 @@ struct BwsLds {
   real Qv[18];         // (Qx, Qu)
   real xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
   alignas(16) real Kst[56];          // results of the last knot, stored one knot later
+  alignas(16) real inv[16];          // Quu^-1 (unsymmetrised), broadcast through LDS
   alignas(16) real dust[4];
   real hx[14], Hs[9], G2v[14];
   real junk[64];       // write target of the spare lanes of a round (never read)
@@ -253,6 +254,9 @@ __device__ __forceinline__ int coef_b(int col) {
 #define MHPC_BWS_CH5 4
 #endif
 constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
+#ifndef MHPC_BWS_INVLDS
+#define MHPC_BWS_INVLDS 1
+#endif
 
 // r2x / r45x: the caller's per-knot side work, run inside the R2 and R45 rounds (before
 // their barriers) so it needs no round of its own -- global traffic of the knot pipeline
@@ -405,8 +409,17 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
   real Qi[16];
   {
     real inv[16];  // unsymmetrised inverse (uniform)
+#if MHPC_BWS_INVLDS
+    // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
+    // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
+    *(lane < 16 ? &sh.inv[lane] : &sh.junk[lane & 63]) = invl;
+    if (NT > 64) __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) inv[e] = sh.inv[e];
+#else
 #pragma unroll
     for (int e = 0; e < 16; ++e) inv[e] = lane_bcast(invl, e);
+#endif
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
