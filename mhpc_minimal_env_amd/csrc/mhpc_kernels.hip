@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "mhpc_device.h"
+#include "mhpc_model_pair.h"
 
 namespace MHPC_NS {
 
@@ -146,15 +147,20 @@ __device__ unsigned long long g_ro_cyc[11];
 // after mhpc_update_problem (receding horizon); otherwise k_cost replaces it.
 // ST = true: the line search reads nominal / gains / references through the LDS stage
 // (requires n_cand >= 10, i.e. <= ST_PPW problems per wave).
-template <bool PIPE, bool ST>
+// PAIR (with PIPE and ST): the dynamics wave gives each candidate a lane pair (even lane
+// front leg, odd lane back leg, mhpc_model_pair.h), 3 problems per block; the cost wave keeps
+// one lane per candidate.  cl = the candidate's lane in the cost wave and in the ring.
+template <bool PIPE, bool ST, bool PAIR>
 __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, DevBufs d,
                                                              int al_iter, int ddp_iter,
                                                              int max_ddp, int full) {
   const int nc = full ? 1 : sp.n_cand;
-  const int ppw = 64 / nc;
+  const int ppw = (PAIR ? 32 : 64) / nc;
   const int t = threadIdx.x, lane = t & 63;
   const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
-  const int lp = lane / nc, j = lane - lp * nc;
+  const int cl = (PAIR && w0) ? (lane >> 1) : lane;
+  const bool back = PAIR && (lane & 1);  // the dynamics lane's leg
+  const int lp = cl / nc, j = cl - lp * nc;
   const int b = blockIdx.x * ppw + lp;
   const bool in = lp < ppw && b < sp.B;
 
@@ -270,7 +276,34 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         const real* nk = ST ? sgp + 2 * (Stage<true>::T0 + kc * TP) : traj_ptr(sp, d, b, nom, ko + k);
         const real* Kk = ST ? sgp + 2 * kc * KP : d.K + ((size_t)b * sp.NK + ko + k) * 56;
         const real* duk = ST ? sgp + 2 * (D0 + 2 * kc) : d.du + ((size_t)b * sp.NK + ko + k) * 4;
-        if (wb) {
+        if (wb && PAIR) {
+          // the own leg's two torques (rows 2 back, 2 back + 1 of K)
+          real u2[2];
+          const int r0 = back ? 2 : 0;
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            real fb = 0;
+#pragma unroll
+            for (int c = 0; c < 14; ++c) fb += Kk[(r0 + ii) * 14 + c] * (x[c] - nk[c]);
+            u2[ii] = (nk[14 + r0 + ii] + eps * duk[r0 + ii]) + fb;
+          }
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk1 = clock64();
+#endif
+          real xd[14], y[4];
+          wb_dynamics_pair(x, u2, mode, back, xd, y);
+#ifdef MHPC_RO_TIMING
+          if (lane == 0) tk2 = clock64() + 0 * xd[13];
+#endif
+          // ring record split over the pair: x[7 back .. 7 back + 6], own u, own-slot y
+#pragma unroll
+          for (int i = 0; i < 7; ++i) rr[i] = back ? x[7 + i] : x[i];
+          rr[7] = u2[0]; rr[8] = u2[1];
+          rr[9] = back ? y[2] : y[0];
+          rr[10] = back ? y[3] : y[1];
+#pragma unroll
+          for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
+        } else if (wb) {
           real u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -314,14 +347,33 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           for (int i = 0; i < 6; ++i) rr[i] = x[i];
 #pragma unroll
           for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = real(0.0); }
+          if (PAIR) {  // the pair splits the 14 record entries: 0..6 even lane, 7..13 odd
+#pragma unroll
+            for (int i = 0; i < 7; ++i) rr[i] = back ? rr[7 + i] : rr[i];
+          }
 #pragma unroll
           for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
         }
       }
       if (PIPE && w0 && run) {
+        if (PAIR) {
+          // WB: x half (7), u pair (2), y pair (2); SRB: half of the 14 entries
+          if (wb) {
 #pragma unroll
-        for (int i = 0; i < RING_W; ++i)
-          if (i < nrec) ring[s][i][lane] = rr[i];
+            for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
+            ring[s][back ? 16 : 14][cl] = rr[7];
+            ring[s][back ? 17 : 15][cl] = rr[8];
+            ring[s][back ? 20 : 18][cl] = rr[9];
+            ring[s][back ? 21 : 19][cl] = rr[10];
+          } else {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < RING_W; ++i)
+            if (i < nrec) ring[s][i][lane] = rr[i];
+        }
       }
       if (PIPE) __syncthreads();
 #ifdef MHPC_RO_TIMING
@@ -353,8 +405,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     if (w0 && run) {
 #pragma unroll
       for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? x[i] : real(0.0);
-      if (PIPE)
+      if (PIPE && PAIR) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          const int e = (back ? 7 : 0) + i;
+          if (e < nx) ring[s][e][cl] = back ? x[7 + i] : x[i];
+        }
+      } else if (PIPE) {
         for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
+      }
       if (wb && p + 1 < sp.P) {
         if (mode == 2 || mode == 4) {
           real xp[14], lam[2];
@@ -1130,8 +1189,8 @@ hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hip
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
                           int max_ddp, int full, hipStream_t s) {
   if (full) {
-    hipLaunchKernelGGL((k_rollout<false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d,
-                       al_iter, 0, 0, 1);
+    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
+                       sp, d, al_iter, 0, 0, 1);
     return hipGetLastError();
   }
   const int ppw = 64 / sp.n_cand;
@@ -1150,18 +1209,30 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
                                      // wave per block only competes for issue slots
 #endif
   const bool st = ppw <= ST_PPW;
-  if (pipe && st)
-    hipLaunchKernelGGL((k_rollout<true, true>), dim3(nblk), dim3(128), 0, s, sp, d, al_iter,
+  // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
+  const int ppw2 = 32 / sp.n_cand;
+  const int nblk2 = ppw2 > 0 ? (sp.B + ppw2 - 1) / ppw2 : 0;
+#ifdef MHPC_RO_PAIR_MAX_BLK
+  const int pair_max = MHPC_RO_PAIR_MAX_BLK;
+#else
+  const int pair_max = 2 * ncu;
+#endif
+  const bool pair = pipe && st && ppw2 > 0 && nblk2 <= pair_max;
+  if (pair)
+    hipLaunchKernelGGL((k_rollout<true, true, true>), dim3(nblk2), dim3(128), 0, s, sp, d, al_iter,
+                       ddp_iter, max_ddp, 0);
+  else if (pipe && st)
+    hipLaunchKernelGGL((k_rollout<true, true, false>), dim3(nblk), dim3(128), 0, s, sp, d, al_iter,
                        ddp_iter, max_ddp, 0);
   else if (pipe)
-    hipLaunchKernelGGL((k_rollout<true, false>), dim3(nblk), dim3(128), 0, s, sp, d, al_iter,
-                       ddp_iter, max_ddp, 0);
+    hipLaunchKernelGGL((k_rollout<true, false, false>), dim3(nblk), dim3(128), 0, s, sp, d,
+                       al_iter, ddp_iter, max_ddp, 0);
   else if (st)
-    hipLaunchKernelGGL((k_rollout<false, true>), dim3(nblk), dim3(64), 0, s, sp, d, al_iter,
-                       ddp_iter, max_ddp, 0);
+    hipLaunchKernelGGL((k_rollout<false, true, false>), dim3(nblk), dim3(64), 0, s, sp, d,
+                       al_iter, ddp_iter, max_ddp, 0);
   else
-    hipLaunchKernelGGL((k_rollout<false, false>), dim3(nblk), dim3(64), 0, s, sp, d, al_iter,
-                       ddp_iter, max_ddp, 0);
+    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3(nblk), dim3(64), 0, s, sp, d,
+                       al_iter, ddp_iter, max_ddp, 0);
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,
