@@ -6,15 +6,23 @@ One step = one full controller solve of the whole per-GPU batch: mhpc_initialize
 `value` = problems solved by all ranks / max-over-ranks wall time of the K timed steps.
 Weak scaling: every rank owns `--batch-per-gpu` independent problems (contiguous shard of
 the global x0 stream); there is no collective in the solve itself, only the barrier and
-max-reduction of the timing contract.
+max-reduction of the timing contract and, after the timed region, the all-gather of the
+per-problem summaries (RCCL) that rank 0 checks against a 1-GPU solve of the global batch.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B]
+  python bench.py --batch-sweep 1,16,64,256,1024,4096,8192     (1 GPU, one line per batch)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself
+(one process per GPU, before anything touches the GPU); under torch.distributed.run it is
+one of them.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,12 +31,71 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6     # MI355X FP64 vector spec (SURVEY.md 8d secondary roofline)
+
+
+# ---------------------------------------------------------------------------------------
+# rank launcher (parent process: never touches the GPU)
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, script: str = None, argv=None) -> int:
+    """Start n ranks of `script` (default: this file with this command line; RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would) and wait for
+    them; the first failing rank's exit code wins and stops the others."""
+    script = script or os.path.abspath(__file__)
+    argv = sys.argv[1:] if argv is None else list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # one rank failed: the collectives would hang the rest
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+# ---------------------------------------------------------------------------------------
+def usable_cpus() -> int:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota (the
+    GPU box gives a job a share of the host; os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def cpu_baseline(desc, opt, sample: int, threads: int, label: str = "C3"):
     """The CPU oracle (restatement of MultiPhaseDDP::solve + the reference's own CasADi
-    kernels, oracle/_ref) on the first `sample` problems of the same workload."""
+    kernels, oracle/_ref) on the first `sample` problems of the same workload, one problem
+    per thread: init+solve, and initialization alone (solve-only = the difference)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import oracle as O
@@ -40,28 +107,120 @@ def cpu_baseline(desc, opt, sample: int, threads: int, label: str = "C3"):
     x0 = configs.x0_for(desc, sample)
     O.solve(desc, opt.to_c(), x0[:min(8, sample)], nthreads=threads)  # warm the page cache
     t0 = time.perf_counter()
+    O.solve(desc, opt.to_c(), x0, nthreads=threads, do_solve=False)
+    t_init = time.perf_counter() - t0
+    t0 = time.perf_counter()
     O.solve(desc, opt.to_c(), x0, nthreads=threads)
     dt = time.perf_counter() - t0
+    solve_only = sample / (dt - t_init) if dt > t_init else None
     return {
         "value": sample / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-        "sample": (f"{sample} {label} problems (same x0 stream), init+solve, CPU restatement of "
-                   f"MultiPhaseDDP::solve calling the reference's own CasADi kernels "
-                   f"(oracle/_ref), g++ -O2, {threads} threads, {dt:.2f} s wall"),
+        "solve_only_per_s": solve_only, "host_cpus": os.cpu_count(),
+        "sample": (f"{sample} {label} problems (same x0 stream), init+solve {dt:.2f} s wall "
+                   f"(initialization alone {t_init:.2f} s), CPU restatement of "
+                   f"MultiPhaseDDP::solve (g++ -O3) calling the reference's own CasADi kernels "
+                   f"(oracle/_ref), one problem per thread on {threads} threads = the CPUs "
+                   f"this job may use (affinity / cgroup quota; the host reports "
+                   f"{os.cpu_count()})"),
     }, None
+
+
+def cpu_sample_for(desc, opt, threads: int, seconds: float) -> int:
+    """Problems for about `seconds` of CPU-baseline work: time a probe of 2 problems per
+    thread and scale (the GPU box's host speed is not known in advance)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    if not O.available():
+        return 0
+    from mhpc_minimal_env_amd import configs
+    n = 2 * threads
+    t0 = time.perf_counter()
+    O.solve(desc, opt.to_c(), configs.x0_for(desc, n), nthreads=threads)
+    per = (time.perf_counter() - t0) / n
+    return int(min(max(seconds / max(per, 1e-6), n), 131072))
 
 
 def load_pmc(kernel: str, batch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
-    batch size (profiles/pmc_traffic_b<batch>.json, tools/pmc_summary.py)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_b{batch}.json")
-    if not os.path.exists(path):
-        return None
+    batch size (profiles/pmc_traffic_b<batch>.json, tools/pmc_summary.py): (bytes, file)."""
+    path = os.path.join("profiles", f"pmc_traffic_b{batch}.json")
+    if not os.path.exists(os.path.join(ROOT, path)):
+        return None, None
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, path)) as f:
             d = json.load(f)
-        return d.get("kernels", {}).get(kernel.split("(")[0], {}).get("hbm_bytes_per_launch")
+        return d.get("kernels", {}).get(kernel.split("(")[0], {}).get("hbm_bytes_per_launch"), path
     except Exception:
-        return None
+        return None, None
+
+
+def roofline_of(stats: dict, batch: int) -> dict:
+    """HBM roofline of the kernel with the largest device time (+ its FP64 VALU rate in the
+    reference's dense flop count, SURVEY.md 8d secondary roofline)."""
+    dom = max(stats, key=lambda k: stats[k]["ms"])
+    ks = stats[dom]
+    per_launch_s = ks["ms"] / 1e3 / max(ks["launches"], 1)
+    bytes_per_launch = ks["alg_bytes"] / max(ks["launches"], 1)
+    flops_per_launch = ks.get("alg_flops", 0.0) / max(ks["launches"], 1)
+    achieved = bytes_per_launch / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    traffic, src = load_pmc(dom, batch)
+    r = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+         "traffic_source": src, "alg_bytes_per_launch": bytes_per_launch,
+         "avg_launch_ms": per_launch_s * 1e3}
+    if flops_per_launch > 0 and per_launch_s > 0:
+        tf = flops_per_launch / per_launch_s / 1e12
+        r["valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": tf / FP64_PEAK_TFS, "alg_flops_per_launch": flops_per_launch,
+                     "flop_model": "reference dense formulation (compute_Qfunction + "
+                                   "valuefunction_update per knot, impact-aware step)"}
+    return r
+
+
+def workload(name: str):
+    from mhpc_minimal_env_amd import configs
+    from mhpc_minimal_env_amd import locomotion as L
+    return getattr(configs, f"{name}_desc")(), L.HSDDP_OPTION()
+
+
+def metric_of(name: str) -> str:
+    return ("MHPC solves/sec (2WB+2SRB trot)" if name == "c3"
+            else "MHPC solves/sec (4WB+6SRB bound)" + (", fp32" if name == "c5f32" else ""))
+
+
+def workload_text(name: str) -> str:
+    return (("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, N=80/phase"
+             if name == "c3" else "C5: Gait() BOUND, 4 WB + 6 SRB, N=80/100 alternating")
+            + ", HSDDP max_AL=2 max_DDP=3; step = initialization + solve of the whole batch")
+
+
+class Solver:
+    """One handle on this rank's GPU, stepping init + solve of its batch."""
+
+    def __init__(self, desc, opt, x0, device):
+        from mhpc_minimal_env_amd import capi
+        from mhpc_minimal_env_amd import locomotion as L
+        self.capi = capi
+        self.loco = L.MHPCLocomotion(desc=desc, option=opt, batch=x0.shape[0], device=device)
+        self.loco.set_initial_condition(x0)
+        self.lib, self.h = capi.lib(), self.loco._h
+        capi.check(self.lib.mhpc_set_x0(self.h, capi.dptr(self.loco._x0)), "mhpc_set_x0")
+
+    def step(self):
+        self.capi.check(self.lib.mhpc_initialize(self.h), "mhpc_initialize")
+        self.capi.check(self.lib.mhpc_solve(self.h, None), "mhpc_solve")
+
+    def summary(self, offset: int):
+        """Per-problem summary of the last solve (sharding.summary_dtype); the status is
+        decoded from the decision trace (abort bit) and the cost."""
+        from mhpc_minimal_env_amd import sharding
+        sc = self.loco.get_scalars()
+        aborted = ((sc["trace"] >> 21) & 1).any(axis=1)
+        status = np.where(aborted, 1, np.where(np.isfinite(sc["J"]), 0, 2)).astype(np.int32)
+        return sharding.make_summary(offset, sc["J"], sc["viol"], status, sc["V"], sc["trace"])
+
+    def close(self):
+        self.loco.close()
 
 
 def run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch):
@@ -138,6 +297,44 @@ def run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch):
         dist.destroy_process_group()
 
 
+def run_sweep(args, torch):
+    """One JSON line per batch size (1 GPU): throughput and the latency of one controller
+    solve (init + solve of the batch; at batch 1 the real-time MPC tick of
+    MHPCLocomotion::solve_mhpc, MHPCLocomotion.cpp:167-195)."""
+    from mhpc_minimal_env_amd import configs
+    desc, opt = workload(args.workload)
+    for B in [int(b) for b in args.batch_sweep.split(",")]:
+        s = Solver(desc, opt, configs.x0_for(desc, B), 0)
+        for _ in range(args.warmup):
+            s.step()
+        s.loco.set_profiling(True)
+        s.loco.reset_kernel_stats()
+        solve_ms = 0.0
+        ddp = 0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            s.step()
+            c = s.loco.get_counters()
+            solve_ms += c["solve_ms"]
+            ddp += c["ddp_iters"]
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        stats = s.loco.kernel_stats()
+        print(json.dumps({
+            "metric": metric_of(args.workload), "batch": B, "value": B * args.steps / dt,
+            "unit": "solves/s", "ms_per_step": dt / args.steps * 1e3,
+            "latency_ms_per_solve_call": dt / args.steps * 1e3,
+            "solve_only_ms": solve_ms / args.steps,
+            "solve_only_per_s": B * args.steps / (solve_ms / 1e3) if solve_ms > 0 else None,
+            "ddp_iters_per_s": ddp / dt, "steps": args.steps, "warmup": args.warmup,
+            "dtype": "f32" if args.workload == "c5f32" else "f64",
+            "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in stats.items()},
+            "roofline": roofline_of(stats, B),
+        }), flush=True)
+        s.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,45 +347,62 @@ def main():
                          "bound solve (fp64), c5f32: the same in the fp32 instantiation "
                          "(BASELINE configs[4]); c2: 256 trial rollouts of one nominal per problem")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="CPU-baseline problems (default: c3 16384, c5 8192)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="CPU-baseline problems (default: ~15 s of CPU work on the usable cores)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU-baseline threads (default: every CPU this job may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shard-check", action="store_true",
+                    help="N > 1: skip rank 0's 1-GPU re-solve of the global batch")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1 process group: nccl = RCCL over xGMI (default); gloo only for "
+                         "tests on a 1-GPU box (with --share-gpu)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="test only: every rank uses GPU 0 (rehearsal of the N-rank path on one GPU)")
+    ap.add_argument("--batch-sweep", default=None,
+                    help="comma-separated batch sizes: one JSON line each (1 GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"# note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
 
     import torch
+    if args.batch_sweep:
+        if world != 1:
+            print("bench.py: --batch-sweep runs on one GPU", file=sys.stderr)
+            sys.exit(2)
+        return run_sweep(args, torch)
     dist = None
+    if args.share_gpu:
+        local_rank = 0
+    # tensors of the timing / gather collectives live where the backend wants them
+    tdev = torch.device(f"cuda:{local_rank}") if args.backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if args.backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=tdev)
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
 
-    from mhpc_minimal_env_amd import capi, configs
-    from mhpc_minimal_env_amd import locomotion as L
+    from mhpc_minimal_env_amd import configs, sharding
 
     B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c5f32": 4096, "c2": 1}[args.workload]
-    desc, opt = getattr(configs, f"{args.workload}_desc")(), L.HSDDP_OPTION()
+    desc, opt = workload(args.workload)
     x0 = configs.x0_for(desc, B, offset=rank * B)
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
-    loco = L.MHPCLocomotion(desc=desc, option=opt, batch=B, device=local_rank)
-    loco.set_initial_condition(x0)
-    lib, h = capi.lib(), loco._h
-
-    def step():
-        capi.check(lib.mhpc_initialize(h), "mhpc_initialize")
-        capi.check(lib.mhpc_solve(h, None), "mhpc_solve")
-
-    capi.check(lib.mhpc_set_x0(h, capi.dptr(loco._x0)), "mhpc_set_x0")
+    s = Solver(desc, opt, x0, local_rank)
     for _ in range(args.warmup):
-        step()
-    loco.set_profiling(True)
-    loco.reset_kernel_stats()
+        s.step()
+    s.loco.set_profiling(True)
+    s.loco.reset_kernel_stats()
 
     def barrier():
         if dist is not None:
@@ -200,49 +414,52 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        c = loco.get_counters()
+        s.step()
+        c = s.loco.get_counters()
         solve_ms += c["solve_ms"]
         ddp_iters += c["ddp_iters"]
     barrier()
     dt = time.perf_counter() - t0
 
-    stats = loco.kernel_stats()
-    tens = torch.tensor([dt, solve_ms / 1e3, float(ddp_iters)], dtype=torch.float64,
-                        device=f"cuda:{local_rank}")
+    stats = s.loco.kernel_stats()
+    tens = torch.tensor([dt, solve_ms / 1e3, float(ddp_iters)], dtype=torch.float64, device=tdev)
+    shard = None
     if dist is not None:
         tmax = tens[:2].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = tens[2:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         dt, solve_s, ddp_total = float(tmax[0]), float(tmax[1]), float(tsum[0])
+        # per-problem summaries of every rank (RCCL all-gather; outside the timed region)
+        allp = sharding.gather_summaries(s.summary(rank * B),
+                                         device=tdev if args.backend == "nccl" else None)
+        shard = {"ranks": dist.get_world_size(), "backend": dist.get_backend(),
+                 "gathered_problems": int(len(allp))}
     else:
         solve_s, ddp_total = solve_ms / 1e3, float(ddp_iters)
+    s.close()
 
     if rank == 0:
+        if shard is not None and not args.no_shard_check:
+            # the same global x0 stream solved on one GPU: every gathered summary must be
+            # bitwise identical
+            one = Solver(desc, opt, configs.x0_for(desc, world * B), local_rank)
+            one.step()
+            ref = one.summary(0)
+            one.close()
+            same = all(np.array_equal(allp[k], ref[k], equal_nan=k != "trace")
+                       for k in ("index", "J", "viol", "status", "V", "trace"))
+            shard["check"] = {"problems": world * B, "bitwise_identical_to_1gpu": bool(same)}
+            if not same:
+                print("bench.py: sharded results differ from the 1-GPU solve", file=sys.stderr)
         total = world * B * args.steps
-        # dominant kernel (largest device time in the timed region) for the roofline
-        dom = max(stats, key=lambda k: stats[k]["ms"])
-        ks = stats[dom]
-        per_launch_s = ks["ms"] / 1e3 / max(ks["launches"], 1)
-        bytes_per_launch = ks["alg_bytes"] / max(ks["launches"], 1)
-        achieved = bytes_per_launch / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-        roofline = {
-            "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_pmc(dom, B), "alg_bytes_per_launch": bytes_per_launch,
-            "avg_launch_ms": per_launch_s * 1e3,
-        }
-        cpu, why = (None, "disabled")
+        cpu, why = (None, "disabled" if world == 1 else "reported at N=1 only")
         if world == 1 and not args.no_cpu_baseline:
-            cpu, why = cpu_baseline(desc, opt, args.cpu_sample or
-                                    (16384 if args.workload == "c3" else 8192),
-                                    min(args.cpu_threads, os.cpu_count() or 1),
-                                    label=args.workload.upper()[:2])
+            threads = args.cpu_threads or usable_cpus()
+            sample = args.cpu_sample or cpu_sample_for(desc, opt, threads, seconds=15.0)
+            cpu, why = cpu_baseline(desc, opt, sample, threads, label=args.workload.upper()[:2])
         line = {
-            "metric": ("MHPC solves/sec (2WB+2SRB trot)" if args.workload == "c3"
-                       else "MHPC solves/sec (4WB+6SRB bound)"
-                       + (", fp32" if args.workload == "c5f32" else "")),
+            "metric": metric_of(args.workload),
             "value": total / dt,
             "unit": "solves/s",
             "n_gpus": world,
@@ -255,11 +472,7 @@ def main():
             "dtype": "f32" if args.workload == "c5f32" else "f64",
             "data": "synthetic (x0 = reference default + splitmix64 perturbation)",
             "config": {
-                "workload": (("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, "
-                              "N=80/phase" if args.workload == "c3" else
-                              "C5: Gait() BOUND, 4 WB + 6 SRB, N=80/100 alternating")
-                             + ", HSDDP max_AL=2 max_DDP=3; step = initialization + solve of "
-                               "the whole batch"),
+                "workload": workload_text(args.workload),
                 "batch_per_gpu": B,
                 "global_batch": world * B,
                 "parallelism": f"batch-sharded x{world}",
@@ -267,12 +480,14 @@ def main():
             "ddp_iters_per_s": ddp_total / dt,
             "solve_only_per_s": total / solve_s if solve_s > 0 else None,
             "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in stats.items()},
-            "roofline": roofline,
+            "roofline": roofline_of(stats, B),
             "cpu_baseline": cpu if cpu is not None else {"value": None, "reason": why},
         }
+        if shard is not None:
+            line["sharding"] = shard
         print(json.dumps(line), flush=True)
-    loco.close()
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

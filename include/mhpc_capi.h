@@ -177,7 +177,28 @@ const char* mhpc_kernel_name(int k);
 int mhpc_set_profiling(mhpc_handle* h, int on);
 int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches, double* alg_bytes);
 int mhpc_reset_kernel_stats(mhpc_handle* h);
+/* Algorithmic FP64 flops per kernel accumulated like mhpc_get_kernel_stats' bytes: the
+ * backward sweep in the reference's dense formulation; 0 for the others. */
+int mhpc_get_kernel_flops(mhpc_handle* h, double* flops);
 void mhpc_destroy(mhpc_handle* h);
+
+/* Kernel variants.  The launch shape of the backward sweep and of the line search is chosen
+ * from the batch size and the device's compute-unit count; every variant
+ * computes the same per-problem arithmetic, bit for bit (tests/test_gpu_variants.py).  This
+ * call pins one variant for the handle's later solves -- for parity tests of every variant
+ * at any batch size, and for tuning.  variant 0 restores the automatic choice.
+ * MHPC_ERR_INVALID if the variant does not apply (the staged line-search variants need at
+ * least 10 line-search candidates, the pair variant at most 32). */
+#define MHPC_VARIANT_BWS 0            /* which: backward sweep */
+#define MHPC_VARIANT_BWS_1WAVE 1      /*   one wave per SIMD, no register cap */
+#define MHPC_VARIANT_BWS_2WAVE 2      /*   256-register build, two waves per SIMD */
+#define MHPC_VARIANT_RO 1             /* which: line-search rollouts */
+#define MHPC_VARIANT_RO_PAIR 1        /*   two-wave pipeline, a lane pair per candidate */
+#define MHPC_VARIANT_RO_PIPE_STAGED 2 /*   two-wave pipeline, LDS-staged operands */
+#define MHPC_VARIANT_RO_PIPE 3        /*   two-wave pipeline, operands from HBM */
+#define MHPC_VARIANT_RO_FUSED_STAGED 4 /*  one wave, LDS-staged operands */
+#define MHPC_VARIANT_RO_FUSED 5       /*   one wave, operands from HBM */
+int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------
  * Replace the CasADi C ABI of SURVEY.md table 2b for whole batches of points.  All
@@ -185,6 +206,17 @@ void mhpc_destroy(mhpc_handle* h);
  * C [n][4][14], D [n][4][4]; SRB Ac [n][6][6], Bc [n][6][4]. */
 int mhpc_eval_wb_dynamics(int device, int n, int mode, const double* x, const double* u,
                           double* xdot, double* y);
+/* The line search's lane-pair evaluation of the same dynamics (mhpc_model_pair.h: even lane
+ * front leg, odd lane back leg): xdot [n][2][14], y [n][2][4] hold what each lane of the pair
+ * computed; both must equal mhpc_eval_wb_dynamics bit for bit. */
+int mhpc_eval_wb_dynamics_pair(int device, int n, int mode, const double* x, const double* u,
+                               double* xdot, double* y);
+/* Touchdown constraint WB_FL1 (foot 0: front, used at the end of mode 2) / WB_FL2 (foot 1:
+ * back, mode 4) and the foot Jacobian Jacob_F / Jacob_B, as the kernels evaluate them:
+ * h [n][2] (the derivative routine's value, then the value-only routine's), hx [n][14],
+ * hxx [n][14][14], J and Jd [n][2][7] (row-major). */
+int mhpc_eval_wb_touchdown(int device, int n, int foot, const double* x, double* h, double* hx,
+                           double* hxx, double* J, double* Jd);
 int mhpc_eval_wb_partials(int device, int n, int mode, const double* x, const double* u,
                           double* Ac, double* Bc, double* C, double* D);
 int mhpc_eval_wb_impact(int device, int n, int foot, const double* x, double* xplus,

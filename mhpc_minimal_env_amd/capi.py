@@ -20,6 +20,13 @@ MHPC_NUM_KERNELS = 6
 MHPC_MAX_ROLLOUT_EPS = 4096
 
 MHPC_OK = 0
+MHPC_ERR_INVALID = 1
+
+# mhpc_set_kernel_variant (include/mhpc_capi.h)
+MHPC_VARIANT_BWS = 0
+MHPC_VARIANT_RO = 1
+BWS_VARIANTS = {"auto": 0, "1wave": 1, "2wave": 2}
+RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged": 4, "fused": 5}
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1
 MHPC_SOLVE_NONFINITE = 2
@@ -134,8 +141,14 @@ SIGNATURES = [
     ("mhpc_get_kernel_stats", ctypes.c_int, [ctypes.c_void_p, _DP,
                                              ctypes.POINTER(ctypes.c_int64), _DP]),
     ("mhpc_reset_kernel_stats", ctypes.c_int, [ctypes.c_void_p]),
+    ("mhpc_get_kernel_flops", ctypes.c_int, [ctypes.c_void_p, _DP]),
+    ("mhpc_set_kernel_variant", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     ("mhpc_eval_wb_dynamics", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                              _DP, _DP]),
+    ("mhpc_eval_wb_dynamics_pair", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP,
+                                                  _DP, _DP, _DP]),
+    ("mhpc_eval_wb_touchdown", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
+                                              _DP, _DP, _DP, _DP]),
     ("mhpc_eval_wb_partials", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                              _DP, _DP, _DP, _DP]),
     ("mhpc_eval_wb_impact", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP, _DP]),

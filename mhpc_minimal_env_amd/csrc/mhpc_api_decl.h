@@ -21,5 +21,7 @@ int api_get_counters(Handle* h, mhpc_counters* c);
 int api_set_profiling(Handle* h, int on);
 int api_get_kernel_stats(Handle* h, double* ms, int64_t* launches, double* alg_bytes);
 int api_reset_kernel_stats(Handle* h);
+int api_get_kernel_flops(Handle* h, double* flops);
+int api_set_kernel_variant(Handle* h, int which, int variant);
 void api_destroy(Handle* h);
 }  // namespace API_NS

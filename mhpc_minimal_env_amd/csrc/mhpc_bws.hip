@@ -413,7 +413,11 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
     // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
     *(lane < 16 ? &sh.inv[lane] : &sh.junk[lane & 63]) = invl;
+    // other lanes' stores become visible: a block barrier across waves; within the single
+    // wave, LDS operations complete in order and the wave barrier keeps the compiler from
+    // moving the loads above the store (no instruction is emitted for it)
     if (NT > 64) __syncthreads();
+    else __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int e = 0; e < 16; ++e) inv[e] = sh.inv[e];
 #else
@@ -985,19 +989,16 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
   }
 }
 
+// Variant: sp.var_bws (mhpc_set_kernel_variant) or, by default, the 1-wave build while the
+// batch fits one wave per SIMD of the handle's device (sp.ncu), the 2-wave build beyond.
+// Both builds compile the same source; tests/test_gpu_variants.py checks them bit for bit.
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, hipStream_t s) {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
 #ifdef MHPC_BWS_WAVES
   hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s, sp,
                      d, update_reg);
 #else
-  if (sp.B <= 4 * ncu)
+  const bool one = sp.var_bws ? sp.var_bws == MHPC_VARIANT_BWS_1WAVE : sp.B <= 4 * sp.ncu;
+  if (one)
     hipLaunchKernelGGL((k_bws<64, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else
     hipLaunchKernelGGL((k_bws<64, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);

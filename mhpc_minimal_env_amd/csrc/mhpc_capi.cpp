@@ -3,6 +3,7 @@
 // mhpc_runtime.cpp according to the descriptor's precision at mhpc_create.
 #include <math.h>
 
+#include <exception>
 #include <string>
 
 #include "../../include/mhpc_capi.h"
@@ -21,14 +22,31 @@ struct mhpc_handle {
   void* impl;
 };
 
-#define FWD(fn, ...)                                                                 \
-  do {                                                                               \
-    if (!h) {                                                                        \
-      mhpc_g_err = "null handle";                                                    \
-      return MHPC_ERR_INVALID;                                                       \
-    }                                                                                \
-    return h->precision == 32 ? mhpc32::api_##fn((mhpc32::Handle*)h->impl, ##__VA_ARGS__) \
-                              : mhpc::api_##fn((mhpc::Handle*)h->impl, ##__VA_ARGS__);   \
+// No exception crosses the ABI: a host allocation failure (std::bad_alloc of a staging
+// vector) or any other exception becomes MHPC_ERR_DEVICE with its message.
+static int fail_exception(const char* fn) {
+  try {
+    throw;
+  } catch (const std::exception& e) {
+    mhpc_g_err = std::string(fn) + ": " + e.what();
+  } catch (...) {
+    mhpc_g_err = std::string(fn) + ": unknown exception";
+  }
+  return MHPC_ERR_DEVICE;
+}
+
+#define FWD(fn, ...)                                                                   \
+  do {                                                                                 \
+    if (!h) {                                                                          \
+      mhpc_g_err = "null handle";                                                      \
+      return MHPC_ERR_INVALID;                                                         \
+    }                                                                                  \
+    try {                                                                              \
+      return h->precision == 32 ? mhpc32::api_##fn((mhpc32::Handle*)h->impl, ##__VA_ARGS__) \
+                                : mhpc::api_##fn((mhpc::Handle*)h->impl, ##__VA_ARGS__);   \
+    } catch (...) {                                                                    \
+      return fail_exception("mhpc_" #fn);                                              \
+    }                                                                                  \
   } while (0)
 
 extern "C" const char* mhpc_version(void) {
@@ -62,17 +80,25 @@ extern "C" int mhpc_create(const mhpc_problem_desc* desc, const mhpc_hsddp_optio
   const int prec = desc->precision;
   void* impl = nullptr;
   int rc;
-  if (prec == 32) {
-    mhpc32::Handle* p = nullptr;
-    rc = mhpc32::api_create(desc, opt, batch, device, &p);
-    impl = p;
-  } else {
-    mhpc::Handle* p = nullptr;
-    rc = mhpc::api_create(desc, opt, batch, device, &p);
-    impl = p;
+  try {
+    if (prec == 32) {
+      mhpc32::Handle* p = nullptr;
+      rc = mhpc32::api_create(desc, opt, batch, device, &p);
+      impl = p;
+    } else {
+      mhpc::Handle* p = nullptr;
+      rc = mhpc::api_create(desc, opt, batch, device, &p);
+      impl = p;
+    }
+    if (rc != MHPC_OK) return rc;
+    *out = new mhpc_handle{prec == 32 ? 32 : 64, impl};
+  } catch (...) {
+    if (impl) {
+      if (prec == 32) mhpc32::api_destroy((mhpc32::Handle*)impl);
+      else mhpc::api_destroy((mhpc::Handle*)impl);
+    }
+    return fail_exception("mhpc_create");
   }
-  if (rc != MHPC_OK) return rc;
-  *out = new mhpc_handle{prec == 32 ? 32 : 64, impl};
   return MHPC_OK;
 }
 
@@ -105,9 +131,17 @@ extern "C" int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launch
   FWD(get_kernel_stats, ms, launches, alg_bytes);
 }
 extern "C" int mhpc_reset_kernel_stats(mhpc_handle* h) { FWD(reset_kernel_stats); }
+extern "C" int mhpc_get_kernel_flops(mhpc_handle* h, double* flops) { FWD(get_kernel_flops, flops); }
+extern "C" int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant) {
+  FWD(set_kernel_variant, which, variant);
+}
 extern "C" void mhpc_destroy(mhpc_handle* h) {
   if (!h) return;
-  if (h->precision == 32) mhpc32::api_destroy((mhpc32::Handle*)h->impl);
-  else mhpc::api_destroy((mhpc::Handle*)h->impl);
+  try {
+    if (h->precision == 32) mhpc32::api_destroy((mhpc32::Handle*)h->impl);
+    else mhpc::api_destroy((mhpc::Handle*)h->impl);
+  } catch (...) {
+    (void)fail_exception("mhpc_destroy");
+  }
   delete h;
 }

@@ -1100,6 +1100,36 @@ __global__ void k_eval_wb_dyn(int n, int mode, const real* x, const real* u, rea
   wb_dynamics<real>(x + (size_t)i * 14, u + (size_t)i * 4, mode, xd + (size_t)i * 14, y + (size_t)i * 4);
 }
 
+// The line search's lane-pair dynamics (mhpc_model_pair.h): lane 2i + leg of point i, both
+// lanes' xdot / y written ([n][2][14], [n][2][4]) so a test can check that each equals the
+// single-lane model.  Lanes past 2n hold whole idle pairs (the DPP swaps stay inside pairs).
+__global__ void k_eval_wb_dyn_pair(int n, int mode, const real* x, const real* u, real* xd,
+                                   real* y) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t >> 1;
+  const bool back = t & 1;
+  if (i >= n) return;
+  const real* xi = x + (size_t)i * 14;
+  const real u2[2] = {u[(size_t)i * 4 + (back ? 2 : 0)], u[(size_t)i * 4 + (back ? 3 : 1)]};
+  real f[14], yy[4];
+  wb_dynamics_pair(xi, u2, mode, back, f, yy);
+  for (int r = 0; r < 14; ++r) xd[(size_t)t * 14 + r] = f[r];
+  for (int r = 0; r < 4; ++r) y[(size_t)t * 4 + r] = yy[r];
+}
+
+// Touchdown constraint (WB_FL1/FL2_terminal_constr) as the kernels evaluate it: h both from
+// the derivative routine (backward sweep) and from the value-only one (line search), hx, hxx;
+// and the foot Jacobian (Jacob_F / Jacob_B) of the PD warm start.
+__global__ void k_eval_wb_aux(int n, int foot, const real* x, real* h, real* hx, real* hxx,
+                              real* J, real* Jd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const real* xi = x + (size_t)i * 14;
+  wb_touchdown(xi, foot, h + (size_t)i * 2, hx + (size_t)i * 14, hxx + (size_t)i * 196);
+  h[(size_t)i * 2 + 1] = foot == kFront ? wb_touchdown_value<kFront>(xi) : wb_touchdown_value<kBack>(xi);
+  wb_foot_jacobian(xi, foot, J + (size_t)i * 14, Jd + (size_t)i * 14);
+}
+
 __global__ void k_eval_wb_par(int n, int mode, const real* x, const real* u, real* Ac,
                               real* Bc, real* C, real* D) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1195,20 +1225,14 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   }
   const int ppw = 64 / sp.n_cand;
   const int nblk = (sp.B + ppw - 1) / ppw;
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
+  const int ncu = sp.ncu;
 #ifdef MHPC_RO_PIPE
-  const bool pipe = MHPC_RO_PIPE;
+  bool pipe = MHPC_RO_PIPE;
 #else
-  const bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
-                                     // wave per block only competes for issue slots
+  bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
+                                // wave per block only competes for issue slots
 #endif
-  const bool st = ppw <= ST_PPW;
+  bool st = ppw <= ST_PPW;
   // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
   const int ppw2 = 32 / sp.n_cand;
   const int nblk2 = ppw2 > 0 ? (sp.B + ppw2 - 1) / ppw2 : 0;
@@ -1217,7 +1241,13 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
 #else
   const int pair_max = 2 * ncu;
 #endif
-  const bool pair = pipe && st && ppw2 > 0 && nblk2 <= pair_max;
+  bool pair = pipe && st && ppw2 > 0 && nblk2 <= pair_max;
+  if (sp.var_ro) {  // forced (mhpc_set_kernel_variant checked that it applies)
+    const int v = sp.var_ro;
+    pair = v == MHPC_VARIANT_RO_PAIR;
+    pipe = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_PIPE;
+    st = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_FUSED_STAGED;
+  }
   if (pair)
     hipLaunchKernelGGL((k_rollout<true, true, true>), dim3(nblk2), dim3(128), 0, s, sp, d, al_iter,
                        ddp_iter, max_ddp, 0);
@@ -1269,6 +1299,18 @@ hipError_t launch_export(const SolveParams& sp, const DevBufs& d, hipStream_t s)
 hipError_t launch_eval_wb_dyn(int n, int mode, const real* x, const real* u, real* xd,
                               real* y, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_wb_dyn, dim3((n + 63) / 64), dim3(64), 0, s, n, mode, x, u, xd, y);
+  return hipGetLastError();
+}
+hipError_t launch_eval_wb_dyn_pair(int n, int mode, const real* x, const real* u, real* xd,
+                                   real* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_eval_wb_dyn_pair, dim3((2 * n + 63) / 64), dim3(64), 0, s, n, mode, x, u, xd,
+                     y);
+  return hipGetLastError();
+}
+hipError_t launch_eval_wb_aux(int n, int foot, const real* x, real* h, real* hx, real* hxx,
+                              real* J, real* Jd, hipStream_t s) {
+  hipLaunchKernelGGL(k_eval_wb_aux, dim3((n + 63) / 64), dim3(64), 0, s, n, foot, x, h, hx, hxx, J,
+                     Jd);
   return hipGetLastError();
 }
 hipError_t launch_eval_wb_par(int n, int mode, const real* x, const real* u, real* Ac,

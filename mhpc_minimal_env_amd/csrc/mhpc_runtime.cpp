@@ -35,6 +35,8 @@ hipError_t launch_reduce_counters(const SolveParams&, const DevBufs&, unsigned l
 hipError_t launch_eval_wb_dyn(int, int, const real*, const real*, real*, real*, hipStream_t);
 hipError_t launch_eval_wb_par(int, int, const real*, const real*, real*, real*, real*,
                               real*, hipStream_t);
+hipError_t launch_eval_wb_dyn_pair(int, int, const real*, const real*, real*, real*, hipStream_t);
+hipError_t launch_eval_wb_aux(int, int, const real*, real*, real*, real*, real*, real*, hipStream_t);
 hipError_t launch_eval_wb_impact(int, int, const real*, real*, real*, hipStream_t);
 hipError_t launch_eval_srb(int, const real*, const real*, const real*, const real*,
                            real*, real*, real*, hipStream_t);
@@ -82,7 +84,7 @@ struct Handle {
   bool profile = false;
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;
-  double kms[NKERN] = {}, kbytes[NKERN] = {};
+  double kms[NKERN] = {}, kbytes[NKERN] = {}, kflops[NKERN] = {};
   int64_t klaunch[NKERN] = {};
   // algorithmic byte model per problem
   double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0, by_cost = 0;
@@ -162,6 +164,13 @@ static void byte_model(Handle* h) {
 static constexpr double kBwsWbKnot = kB * (PS + 22 + 1 + 56 + 4 + 14);
 static constexpr double kBwsFbKnot = kB * (10 + 1 + 24 + 4 + 6);
 static constexpr double kBwsPx = kB * 196;
+// Algorithmic FP64 flops of the backward sweep in the reference's dense formulation
+// (compute_Qfunction 20.2k + valuefunction_update 4.3k per WB knot,
+// ~3k per SRB knot; impact_aware_step Px' G, Px' H Px: 2 (2 * 14^3) + 2 * 14^2).  The
+// kernel skips the structural zeros, so this is the dense-equivalent rate, an upper bound
+// on the flops it executes.
+static constexpr double kFlopWbKnot = 24.5e3, kFlopFbKnot = 3.0e3,
+                        kFlopPx = 2.0 * (2.0 * 14 * 14 * 14) + 2.0 * 14 * 14;
 
 const char* api_kernel_name(int k) {
   return (k >= 0 && k < NKERN) ? kKernelNames[k] : "";
@@ -215,6 +224,10 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   memset(&sp, 0, sizeof sp);
   sp.B = batch;
   layout_params(sp, *desc);
+  // launch shapes follow this handle's device (one process may hold handles on several)
+  if (hipDeviceGetAttribute(&sp.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      sp.ncu < 1)
+    sp.ncu = 256;
   for (int p = 0; p < sp.P; ++p) sp.buf[p] = p;
   sp.vel = desc->vel_cmd;
   sp.height = desc->height_cmd;
@@ -435,11 +448,24 @@ int api_solve(Handle* h, int32_t* status) {
   h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
   h->kbytes[K_BWS] += c[C_BWS_KNOTS_WB] * kBwsWbKnot + c[C_BWS_KNOTS_FB] * kBwsFbKnot +
                       c[C_PX_READS] * kBwsPx;
+  h->kflops[K_BWS] += c[C_BWS_KNOTS_WB] * kFlopWbKnot + c[C_BWS_KNOTS_FB] * kFlopFbKnot +
+                      c[C_PX_READS] * kFlopPx;
   if (status) {
     std::vector<ProbState> st(h->sp.B);
     D2H(st.data(), h->d.st, st.size() * sizeof(ProbState));
     for (int b = 0; b < h->sp.B; ++b) status[b] = st[b].status;
   }
+  return MHPC_OK;
+}
+
+// Rows [ko, ko + N) of a problem-major [B][NK][per] device array into buf ([B][N][per]):
+// one strided copy of just the requested phase (not the whole trajectory buffer).
+static int copy_rows(Handle* h, const real* src, int per, int ko, int N, std::vector<real>& buf) {
+  const size_t B = h->sp.B, NK = h->sp.NK, w = (size_t)N * per * sizeof(real);
+  buf.resize(B * N * per);
+  HIPCHK(hipMemcpy2DAsync(buf.data(), w, src + (size_t)ko * per, NK * per * sizeof(real), w, B,
+                          hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
   return MHPC_OK;
 }
 
@@ -450,17 +476,16 @@ int api_get_phase(Handle* h, int phase, double* x, double* u, double* y,
   const SolveParams& sp = h->sp;
   if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
   HIPCHK(hipSetDevice(h->device));
-  const size_t B = sp.B, NK = sp.NK;
+  const size_t B = sp.B;
   const int n = sp.xs[phase], N = sp.N[phase], ko = sp.ko[phase];
+  std::vector<real> buf;
+  int rc;
   if (x || u || y) {
     HIPCHK(launch_export(sp, h->d, h->stream));
-    std::vector<real> buf(B * NK * KS);
-    HIPCHK(hipMemcpyAsync(buf.data(), h->d.out, buf.size() * sizeof(real), hipMemcpyDeviceToHost,
-                          h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if ((rc = copy_rows(h, h->d.out, KS, ko, N, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k) {
-        const real* r = &buf[(b * NK + ko + k) * KS];
+        const real* r = &buf[(b * N + k) * KS];
         for (int i = 0; i < n; ++i)
           if (x) x[(b * N + k) * n + i] = r[i];
         for (int i = 0; i < 4; ++i) {
@@ -470,25 +495,20 @@ int api_get_phase(Handle* h, int phase, double* x, double* u, double* y,
       }
   }
   if (K) {
-    std::vector<real> buf(B * NK * 56);
-    D2H(buf.data(), h->d.K, buf.size() * sizeof(real));
+    if ((rc = copy_rows(h, h->d.K, 56, ko, N, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
-        for (int i = 0; i < 4 * n; ++i) K[(b * N + k) * 4 * n + i] = buf[(b * NK + ko + k) * 56 + i];
+        for (int i = 0; i < 4 * n; ++i) K[(b * N + k) * 4 * n + i] = buf[(b * N + k) * 56 + i];
   }
   if (du) {
-    std::vector<real> buf(B * NK * 4);
-    D2H(buf.data(), h->d.du, buf.size() * sizeof(real));
-    for (size_t b = 0; b < B; ++b)
-      for (int k = 0; k < N; ++k)
-        for (int i = 0; i < 4; ++i) du[(b * N + k) * 4 + i] = buf[(b * NK + ko + k) * 4 + i];
+    if ((rc = copy_rows(h, h->d.du, 4, ko, N, buf))) return rc;
+    for (size_t i = 0; i < B * N * 4; ++i) du[i] = buf[i];
   }
   if (Vx) {
-    std::vector<real> buf(B * NK * 14);
-    D2H(buf.data(), h->d.G, buf.size() * sizeof(real));
+    if ((rc = copy_rows(h, h->d.G, 14, ko, N, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
-        for (int i = 0; i < n; ++i) Vx[(b * N + k) * n + i] = buf[(b * NK + ko + k) * 14 + i];
+        for (int i = 0; i < n; ++i) Vx[(b * N + k) * n + i] = buf[(b * N + k) * 14 + i];
   }
   return MHPC_OK;
 }
@@ -687,9 +707,37 @@ int api_get_kernel_stats(Handle* h, double* ms, int64_t* launches,
   return MHPC_OK;
 }
 
+int api_set_kernel_variant(Handle* h, int which, int variant) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  SolveParams& sp = h->sp;
+  if (which == MHPC_VARIANT_BWS) {
+    if (variant < 0 || variant > MHPC_VARIANT_BWS_2WAVE) return fail(MHPC_ERR_INVALID, "no such backward-sweep variant");
+    sp.var_bws = variant;
+    return MHPC_OK;
+  }
+  if (which != MHPC_VARIANT_RO) return fail(MHPC_ERR_INVALID, "no such kernel");
+  if (variant < 0 || variant > MHPC_VARIANT_RO_FUSED) return fail(MHPC_ERR_INVALID, "no such line-search variant");
+  const bool staged = variant == MHPC_VARIANT_RO_PAIR || variant == MHPC_VARIANT_RO_PIPE_STAGED ||
+                      variant == MHPC_VARIANT_RO_FUSED_STAGED;
+  if (staged && 64 / sp.n_cand > 6)  // ST_PPW problems per staged wave (mhpc_kernels.hip)
+    return fail(MHPC_ERR_INVALID, "staged line-search variants need >= 10 candidates");
+  if (variant == MHPC_VARIANT_RO_PAIR && 32 / sp.n_cand < 1)
+    return fail(MHPC_ERR_INVALID, "the pair variant needs <= 32 candidates");
+  sp.var_ro = variant;
+  return MHPC_OK;
+}
+
+int api_get_kernel_flops(Handle* h, double* flops) {
+  if (!h || !flops) return fail(MHPC_ERR_INVALID, "null argument");
+  for (int k = 0; k < NKERN; ++k) flops[k] = h->kflops[k];
+  return MHPC_OK;
+}
+
 int api_reset_kernel_stats(Handle* h) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
-  for (int k = 0; k < NKERN; ++k) { h->kms[k] = 0; h->kbytes[k] = 0; h->klaunch[k] = 0; }
+  for (int k = 0; k < NKERN; ++k) {
+    h->kms[k] = 0; h->kbytes[k] = 0; h->kflops[k] = 0; h->klaunch[k] = 0;
+  }
   return MHPC_OK;
 }
 
@@ -738,6 +786,42 @@ extern "C" int mhpc_eval_wb_dynamics(int device, int n, int mode, const double* 
   HIPCHK(launch_eval_wb_dyn(n, mode, dx, du, dxd, dy, nullptr));
   HIPCHK(hipMemcpy(xdot, dxd, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(y, dy, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_eval_wb_dynamics_pair(int device, int n, int mode, const double* x,
+                                          const double* u, double* xdot, double* y) {
+  if (n < 1 || !x || !u || !xdot || !y || mode < 1 || mode > 4)
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 14, &e), *du = s.put(u, n * 4, &e);
+  double *dxd = s.put(nullptr, n * 28, &e), *dy = s.put(nullptr, n * 8, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_wb_dyn_pair(n, mode, dx, du, dxd, dy, nullptr));
+  HIPCHK(hipMemcpy(xdot, dxd, n * 28 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(y, dy, n * 8 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+
+extern "C" int mhpc_eval_wb_touchdown(int device, int n, int foot, const double* x, double* h,
+                                      double* hx, double* hxx, double* J, double* Jd) {
+  if (n < 1 || !x || !h || !hx || !hxx || !J || !Jd || (foot != 0 && foot != 1))
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  DevScratch s;
+  hipError_t e = hipSuccess;
+  double *dx = s.put(x, n * 14, &e), *dh = s.put(nullptr, n * 2, &e);
+  double *dhx = s.put(nullptr, n * 14, &e), *dhxx = s.put(nullptr, n * 196, &e);
+  double *dJ = s.put(nullptr, n * 14, &e), *dJd = s.put(nullptr, n * 14, &e);
+  HIPCHK(e);
+  HIPCHK(launch_eval_wb_aux(n, foot, dx, dh, dhx, dhxx, dJ, dJd, nullptr));
+  HIPCHK(hipMemcpy(h, dh, n * 2 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hx, dhx, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hxx, dhxx, n * 196 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(J, dJ, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Jd, dJd, n * 14 * sizeof(double), hipMemcpyDeviceToHost));
   return MHPC_OK;
 }
 

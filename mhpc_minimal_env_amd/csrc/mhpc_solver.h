@@ -59,6 +59,9 @@ struct SolveParams {
   // configuration directions (+ the impact directions) and velocity / control directions
   int par_items, par_items_v;
   int par_item_off[MAXP + 1], par_v_off[MAXP + 1];
+  // launch shape (host side only): compute units of the handle's device and the kernel
+  // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
+  int ncu, var_bws, var_ro;
 };
 
 struct ProbState {

@@ -333,12 +333,24 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_get_kernel_stats(
             self._h, capi.dptr(ms), nl.ctypes.data_as(__import__("ctypes").POINTER(
                 __import__("ctypes").c_int64)), capi.dptr(by)), "mhpc_get_kernel_stats")
+        fl = np.zeros(n)
+        capi.check(capi.lib().mhpc_get_kernel_flops(self._h, capi.dptr(fl)), "mhpc_get_kernel_flops")
         return {capi.lib().mhpc_kernel_name(k).decode(): {"ms": float(ms[k]), "launches": int(nl[k]),
-                                                          "alg_bytes": float(by[k])}
+                                                          "alg_bytes": float(by[k]),
+                                                          "alg_flops": float(fl[k])}
                 for k in range(n)}
 
     def reset_kernel_stats(self):
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
+
+    def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto"):
+        """Pin the backward-sweep / line-search launch variant (mhpc_set_kernel_variant);
+        names in capi.BWS_VARIANTS / capi.RO_VARIANTS, "auto" = chosen by batch size."""
+        L = capi.lib()
+        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_BWS,
+                                             capi.BWS_VARIANTS[bws]), "mhpc_set_kernel_variant")
+        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO,
+                                             capi.RO_VARIANTS[rollout]), "mhpc_set_kernel_variant")
 
     def concatenated(self) -> dict:
         """Phase-concatenated per-problem arrays (the oracle's layout)."""

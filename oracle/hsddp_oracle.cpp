@@ -650,7 +650,7 @@ void compute_Qfunction(CTG& c, const RCost& rc, const Par& p, const double* Gn, 
 
 // CostToGoStruct::valuefunction_update (MHPC_CompoundTypes.h:128-144)
 double valuefunction_update(CTG& c, int n) {
-  double inv[16], Qi[16], t[56], w[56];
+  double inv[16], Qi[16], t[56], w[196];
   inverse4(c.Quu, inv);
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) Qi[i * 4 + j] = (inv[i * 4 + j] + inv[j * 4 + i]) / 2;

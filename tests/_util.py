@@ -9,8 +9,10 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # with an identical decision trace.  The model arithmetic differs from CasADi's QR at
 # ~1e-11 relative (tests/test_model_host.py), which the solve amplifies to <~1e-8.
 SOLVE_TOL = 1e-6
-# per-function tolerance of the hand-written model vs the CasADi kernels
-KAT_TOL = {"value": 1e-9, "jac": 1e-7}
+# per-function tolerance of the hand-written model vs the CasADi kernels.  Measured worst
+# cases over the 64 KAT states (host build, tests/test_model_host.py): values 1.5e-10
+# (Dyn_FL, Imp_B), Jacobians 1.4e-9 (Dyn_FL_par); CasADi's QR leaves ~1e-10 noise itself.
+KAT_TOL = {"value": 1e-9, "jac": 5e-9}
 
 
 def golden(name):

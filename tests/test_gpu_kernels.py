@@ -60,3 +60,39 @@ def test_srb_bit_exact(kat, L):
     np.testing.assert_array_equal(xd, kat["FBDynamics.xdot"])
     np.testing.assert_array_equal(A, kat["FBDynamics_par.Ac"])
     np.testing.assert_array_equal(B, kat["FBDynamics_par.Bc"])
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_wb_dynamics_pair_bitwise(kat, L, mode):
+    """The line search's lane-pair dynamics (mhpc_model_pair.h) reproduces the single-lane
+    model bit for bit on both lanes of every pair (so forward_sweep(0) as a cost evaluation
+    of the stored nominal stays exact whichever rollout variant produced it)."""
+    x, u = kat["x"], kat["u"]
+    n = len(x)
+    xd, y = np.zeros((n, 14)), np.zeros((n, 4))
+    L.check(L.lib().mhpc_eval_wb_dynamics(0, n, mode, L.dptr(x), L.dptr(u), L.dptr(xd), L.dptr(y)))
+    xd2, y2 = np.zeros((n, 2, 14)), np.zeros((n, 2, 4))
+    L.check(L.lib().mhpc_eval_wb_dynamics_pair(0, n, mode, L.dptr(x), L.dptr(u), L.dptr(xd2),
+                                               L.dptr(y2)))
+    for lane in (0, 1):
+        np.testing.assert_array_equal(xd2[:, lane], xd, err_msg=f"lane {lane} xdot")
+        np.testing.assert_array_equal(y2[:, lane], y, err_msg=f"lane {lane} y")
+
+
+@pytest.mark.parametrize("foot,td,jac", [(0, "WB_FL1_terminal_constr", "Jacob_F"),
+                                         (1, "WB_FL2_terminal_constr", "Jacob_B")])
+def test_touchdown_and_foot_jacobian(kat, L, foot, td, jac):
+    """Touchdown constraint (MHPCConstraints.cpp:91-107) and foot Jacobian
+    (PlanarQuadruped.cpp:103-117) on the device vs the reference's CasADi kernels."""
+    x = kat["x"]
+    n = len(x)
+    h, hx, hxx = np.zeros((n, 2)), np.zeros((n, 14)), np.zeros((n, 14, 14))
+    J, Jd = np.zeros((n, 2, 7)), np.zeros((n, 2, 7))
+    L.check(L.lib().mhpc_eval_wb_touchdown(0, n, foot, L.dptr(x), L.dptr(h), L.dptr(hx),
+                                           L.dptr(hxx), L.dptr(J), L.dptr(Jd)))
+    np.testing.assert_array_equal(h[:, 0], h[:, 1])  # line search and backward sweep agree
+    assert np.max(np.abs(h[:, 0] - kat[td + ".h"])) < 1e-14
+    assert rel_err(hx, kat[td + ".hx"]) < 1e-14
+    assert rel_err(hxx, kat[td + ".hxx"]) < 1e-14
+    assert rel_err(J, kat[jac + ".J"]) < 1e-14
+    assert rel_err(Jd, kat[jac + ".Jd"]) < 1e-13
