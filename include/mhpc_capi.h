@@ -217,6 +217,11 @@ int mhpc_eval_wb_dynamics_pair(int device, int n, int mode, const double* x, con
  * hxx [n][14][14], J and Jd [n][2][7] (row-major). */
 int mhpc_eval_wb_touchdown(int device, int n, int foot, const double* x, double* h, double* hx,
                            double* hxx, double* J, double* Jd);
+/* The same two models in the fp32 instantiation (config C5): pair = 0 single lane (xdot
+ * [n][14], y [n][4]), pair = 1 lane pair (xdot [n][2][14], y [n][2][4]); double host arrays,
+ * inputs rounded to float. */
+int mhpc_eval_wb_dynamics_f32(int device, int n, int mode, int pair, const double* x,
+                              const double* u, double* xdot, double* y);
 int mhpc_eval_wb_partials(int device, int n, int mode, const double* x, const double* u,
                           double* Ac, double* Bc, double* C, double* D);
 int mhpc_eval_wb_impact(int device, int n, int foot, const double* x, double* xplus,

@@ -149,6 +149,8 @@ SIGNATURES = [
                                                   _DP, _DP, _DP]),
     ("mhpc_eval_wb_touchdown", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                               _DP, _DP, _DP, _DP]),
+    ("mhpc_eval_wb_dynamics_f32", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, _DP, _DP, _DP, _DP]),
     ("mhpc_eval_wb_partials", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                              _DP, _DP, _DP, _DP]),
     ("mhpc_eval_wb_impact", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP, _DP]),

@@ -412,12 +412,25 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
 #if MHPC_BWS_INVLDS
     // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
     // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
+    // Lanes 0..15 store, every lane reads all 16 back, within one wave (NT == 64): the
+    // wave's LDS operations complete in issue order, and the compiler keeps the loads
+    // behind the store because they may alias it (same array, lane-dependent index).  Any
+    // explicit ordering costs: a wave barrier (a scheduling barrier) +9 % backward-sweep
+    // time, wavefront-scope fences +9 %, volatile accesses +28 % (MHPC_BWS_WAVEBAR = 1 / 3
+    // builds; A/B at batch 1024 in profiles/r02_ab_inverse_broadcast.txt).
+#ifndef MHPC_BWS_WAVEBAR
+#define MHPC_BWS_WAVEBAR 0
+#endif
     *(lane < 16 ? &sh.inv[lane] : &sh.junk[lane & 63]) = invl;
-    // other lanes' stores become visible: a block barrier across waves; within the single
-    // wave, LDS operations complete in order and the wave barrier keeps the compiler from
-    // moving the loads above the store (no instruction is emitted for it)
     if (NT > 64) __syncthreads();
+#if MHPC_BWS_WAVEBAR == 1
     else __builtin_amdgcn_wave_barrier();
+#elif MHPC_BWS_WAVEBAR == 3
+    else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#endif
 #pragma unroll
     for (int e = 0; e < 16; ++e) inv[e] = sh.inv[e];
 #else

@@ -56,6 +56,7 @@ static __device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (
 // values this path never sees.  The line search evaluates up to 11 of these per WB knot
 // and candidate while the ReB barrier is active.
 static __device__ __forceinline__ real log_pos(real x) {
+  MHPC_NO_FMA_F32
 #ifdef MHPC_FP32
   return logf(x);
 #else
@@ -86,6 +87,7 @@ static __device__ __forceinline__ real log_pos(real x) {
 // NaN, as pow defines), pow(g, -2) = 1/(g*g) (within 1 ulp of the correctly rounded value).
 static __device__ __forceinline__ void reduced_barrier(real g, real delta, real* B, real* Bz,
                                                 real* Bzz) {
+  MHPC_NO_FMA_F32
   if (g > delta) {
     *B = -log_pos(g);
     *Bz = -1.0 / g;
@@ -103,6 +105,7 @@ static __device__ __forceinline__ void reduced_barrier(real g, real delta, real*
 static __device__ real wb_running_cost(const SolveParams& sp, int mode, real dt, real pos,
                                   const real* x, const real* u, const real* y, bool reb,
                                   real delta, real eps_tq, real eps_grf) {
+  MHPC_NO_FMA_F32
   const int m = mode - 1;
   real rx[14] = {pos, sp.height, 0, cQjointBias[0], cQjointBias[1], cQjointBias[2],
                    cQjointBias[3], sp.vel, 0, 0, 0, 0, 0, 0};
@@ -142,6 +145,7 @@ static __device__ real wb_running_cost(const SolveParams& sp, int mode, real dt,
 
 static __device__ real fb_running_cost(const SolveParams& sp, int mode, real dt, real pos,
                                   const real* x, const real* u) {
+  MHPC_NO_FMA_F32
   const int m = mode - 1;
   const real rx[6] = {pos, sp.height, 0, sp.vel, 0, 0};
   const real ru[4] = {0, kGRF, 0, kGRF};
@@ -208,6 +212,7 @@ static __device__ void wb_cost_uy_derivs(int mode, real dt, const real* u, const
 }
 
 static __device__ void wb_term_ref(const SolveParams& sp, int mode, real pos, real* rx) {
+  MHPC_NO_FMA_F32
 #pragma unroll
   for (int i = 0; i < 14; ++i) rx[i] = cXtermWB[mode - 1][i];
   rx[7] = sp.vel;
@@ -215,12 +220,14 @@ static __device__ void wb_term_ref(const SolveParams& sp, int mode, real pos, re
 }
 
 static __device__ void fb_term_ref(const SolveParams& sp, real pos, real* rx) {
+  MHPC_NO_FMA_F32
   rx[0] = pos; rx[1] = sp.height; rx[2] = 0; rx[3] = sp.vel; rx[4] = 0; rx[5] = 0;
 }
 
 // FootholdPlanner::get_foothold_location (FootholdPlan.h:26-50), velcmd 1.5 / ground
 // -0.404 hard-coded by the reference (MHPCLocomotion.cpp:25).
 static __device__ void plan_foothold(const real* x0, real stance_time, int mode, real* f) {
+  MHPC_NO_FMA_F32
   f[0] = f[1] = f[2] = f[3] = 0;
   if (mode == 1) {
     f[2] = (cos(x0[2]) * (-real(0.19)) + x0[0]) + real(1.5) * stance_time / 2;

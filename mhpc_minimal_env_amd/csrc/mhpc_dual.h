@@ -23,6 +23,18 @@
 #define MHPC_NO_FMA
 #endif
 
+// fp32 build only: no contraction in the line search and the cost functions.  In fp32 the
+// SLP vectorizer packs scalar operations into v_pk_* pairs differently in each line-search
+// variant, and a packed multiply loses the contract flag of a scalar one, so the same
+// expression would fuse in one variant and not in another; with no contraction the rounding
+// is the same whatever is packed (tests/test_gpu_variants.py, fp32).  fp64 has no packed
+// arithmetic on gfx950, so its contraction is the same in every variant.
+#if defined(__clang__) && defined(MHPC_FP32)
+#define MHPC_NO_FMA_F32 _Pragma("clang fp contract(off)")
+#else
+#define MHPC_NO_FMA_F32
+#endif
+
 namespace MHPC_NS {
 
 struct Dual {

@@ -21,8 +21,24 @@
 //
 // Everything is templated on the scalar so the same source runs in real (rollouts)
 // and in Dual (one Jacobian column per lane).
+//
+// No FMA contraction in the whole-body functions below (MHPC_NO_FMA): the line search's
+// lane-pair model (mhpc_model_pair.h) forms each leg's terms on its own lane and sums them
+// after a lane swap, where a product cannot fuse into the sum; with every product rounded
+// in both models the result depends only on the order of operations, which the two share,
+// so they agree bit for bit (tests/test_gpu_kernels.py::test_wb_dynamics_pair_bitwise,
+// tests/test_pair_host.py) and a problem's result does not depend on which line-search
+// variant its batch size selects.
 #pragma once
 #include "mhpc_dual.h"
+
+// MHPC_WB_FMA (timing experiments only) lets the compiler contract the whole-body model
+// again; the line-search variants then no longer agree bit for bit.
+#ifdef MHPC_WB_FMA
+#define MHPC_NO_FMA_WB
+#else
+#define MHPC_NO_FMA_WB MHPC_NO_FMA
+#endif
 
 namespace MHPC_NS {
 
@@ -98,6 +114,7 @@ MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g) {
 template <class Q, class V, int F>
 MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, real l1, real l2, Q jx[5], Q jz[5], V* jdx,
                            V* jdz) {
+  MHPC_NO_FMA_WB
   constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   const LegGeo<Q, V>& L = g.leg[F];
   // d/da of l*(-sin a, -cos a) = l*(-cos a, sin a)
@@ -120,6 +137,7 @@ MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // Contribution of the thigh and shank of leg F to M (packed) and h.  xv = qdot.
 template <class Q, class V, int F>
 MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
+  MHPC_NO_FMA_WB
   constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
   const V thd2 = xv[2] * xv[2];
@@ -188,6 +206,7 @@ struct ArrowFactor {
 
 template <class S>
 MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
+  MHPC_NO_FMA_WB
   // base Schur complement S = Mbb - sum_l Mlb' Ml^-1 Mlb (symmetric, lower packed)
   S s00 = M[tri(0, 0)], s10 = M[tri(1, 0)], s11 = M[tri(1, 1)];
   S s20 = M[tri(2, 0)], s21 = M[tri(2, 1)], s22 = M[tri(2, 2)];
@@ -231,6 +250,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
 // b <- M^-1 b  (M, factor in Q; b in V)
 template <class Q, class V>
 MHPC_HD void arrow_solve(const Q M[28], const ArrowFactor<Q>& F, V b[7]) {
+  MHPC_NO_FMA_WB
   V w[2][2];
   V r0 = b[0], r1 = b[1], r2 = b[2];
 #pragma unroll
@@ -258,6 +278,7 @@ MHPC_HD void arrow_solve(const Q M[28], const ArrowFactor<Q>& F, V b[7]) {
 // Foot Jacobian (2x7, dense) and Jdot*qdot of foot F.  xv = qdot.
 template <class Q, class V, int F>
 MHPC_HD void wb_foot_jac_full(const V* xv, const WbGeo<Q, V>& g, Q J[2][7], V jd[2]) {
+  MHPC_NO_FMA_WB
   Q jx[5], jz[5];
   V jdx, jdz;
   leg_point_jac<Q, V, F>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
@@ -278,6 +299,7 @@ MHPC_HD void wb_foot_jac_full(const V* xv, const WbGeo<Q, V>& g, Q J[2][7], V jd
 template <class Q, class V>
 MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7], const V c[2],
                          V v[7], V lam[2]) {
+  MHPC_NO_FMA_WB
   Q Y[2][7];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -353,6 +375,7 @@ MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
 // q+ = q, [M -J'; J 0][qd+; Lam] = [M qd-; 0].
 template <class S, int F>
 MHPC_HD void wb_impact_f(const S* x, S* xp, S* Lam) {
+  MHPC_NO_FMA_F32
   WbGeo<S, S> g;
   wb_geometry<S, S>(x, x + 7, g);
   S M[28], h[7];
@@ -385,6 +408,7 @@ MHPC_HD void wb_impact(const S* x, int f, S* xp, S* Lam) {
 // the state indices (theta, hip, knee) of that leg.
 template <int F>
 MHPC_HD real wb_touchdown_value(const real* x) {
+  MHPC_NO_FMA_F32
   constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int ih = 3 + 2 * F, ik = 4 + 2 * F;
   const real a1 = x[2] + x[ih];

@@ -8,8 +8,10 @@
 // swaps the per-leg terms of those shared quantities with one DPP move per word; both lanes
 // then sum them in the order of the single-lane model (front thigh, front shank, back thigh,
 // back shank; front leg before back leg), so every result -- and the base state both lanes
-// carry -- is the single-lane model's value, bit for bit where the compiler contracts the
-// same expressions (tests/test_gpu_kernels.py: wb_dynamics vs the pair on random states).
+// carry -- is the single-lane model's value, bit for bit: neither model contracts a
+// product into a sum (MHPC_NO_FMA, see mhpc_model.h), so equal operation order means equal
+// rounding (tests/test_pair_host.py emulates the pair on the host with two threads;
+// tests/test_gpu_kernels.py::test_wb_dynamics_pair_bitwise checks the device code).
 // About 40 % fewer instructions per lane than one lane evaluating the whole model.
 #pragma once
 #include "mhpc_model.h"
@@ -18,20 +20,24 @@ namespace MHPC_NS {
 
 // value held by the partner lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2] (device only; the
 // host pass of the kernels' translation unit only parses it)
-__device__ __forceinline__ double pair_swap(double v) {
+MHPC_HD double pair_swap(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
   const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, 0xB1, 0xF, 0xF, false);
   const unsigned hi =
       (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), 0xB1, 0xF, 0xF, false);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+#elif defined(MHPC_PAIR_HOST_SWAP)
+  return mhpc_host_pair_swap(v);  // test-only host emulation of the lane pair (two threads)
 #else
   return v;
 #endif
 }
-__device__ __forceinline__ float pair_swap(float v) {
+MHPC_HD float pair_swap(float v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+#elif defined(MHPC_PAIR_HOST_SWAP)
+  return (float)mhpc_host_pair_swap((double)v);
 #else
   return v;
 #endif
@@ -39,9 +45,10 @@ __device__ __forceinline__ float pair_swap(float v) {
 
 // Jacobian of a point of the own leg (leg_point_jac with the hip side as data: sg = +1
 // front, -1 back), same expressions.
-__device__ __forceinline__ void pair_point_jac(const LegGeo<real, real>& L, real sg, real sth,
+MHPC_HD void pair_point_jac(const LegGeo<real, real>& L, real sg, real sth,
                                                real cth, real l1, real l2, real jx[5], real jz[5],
                                                real* jdx, real* jdz) {
+  MHPC_NO_FMA_WB
   const real tx1 = -l1 * L.c1, tz1 = l1 * L.s1;
   const real tx2 = -l2 * L.c2, tz2 = l2 * L.s2;
   jx[0] = real(1.0); jz[0] = real(0.0);
@@ -65,8 +72,9 @@ struct PairLegMH {
   real Mhh, Mkh, Mkk;  // leg block
   real hh, hk;         // h of the hip / knee joint
 };
-__device__ __forceinline__ void pair_leg_mass_bias(const LegGeo<real, real>& L, real sg, real sth,
+MHPC_HD void pair_leg_mass_bias(const LegGeo<real, real>& L, real sg, real sth,
                                                    real cth, real thd, PairLegMH& o) {
+  MHPC_NO_FMA_WB  // as add_leg (mhpc_model.h): the per-body terms are rounded before any sum
   const real thd2 = thd * thd;
   const real hax = (-sg * kHipX) * cth * thd2;
   const real haz = (sg * kHipX) * sth * thd2;
@@ -117,7 +125,7 @@ __device__ __forceinline__ void pair_leg_mass_bias(const LegGeo<real, real>& L, 
 }
 
 // Order the own / partner value of a per-leg quantity as (front, back).
-__device__ __forceinline__ void pair_order(bool back, real own, real* fr, real* bk) {
+MHPC_HD void pair_order(bool back, real own, real* fr, real* bk) {
   const real oth = pair_swap(own);
   *fr = back ? oth : own;
   *bk = back ? own : oth;
@@ -132,8 +140,9 @@ struct PairFactor {
   real Si[6];      // inverse base Schur complement (identical on both lanes)
   real Mh[3], Mk[3];  // own coupling rows (M(i0, j), M(i1, j))
 };
-__device__ __forceinline__ void pair_solve(const PairFactor& F, bool back, const real rb[3],
+MHPC_HD void pair_solve(const PairFactor& F, bool back, const real rb[3],
                                            const real rl[2], real xb[3], real xl[2]) {
+  MHPC_NO_FMA_WB
   const real w0 = F.Li[0] * rl[0] + F.Li[1] * rl[1];
   const real w1 = F.Li[1] * rl[0] + F.Li[2] * rl[1];
   const real t0 = F.Mh[0] * w0 + F.Mk[0] * w1;
@@ -156,8 +165,9 @@ __device__ __forceinline__ void pair_solve(const PairFactor& F, bool back, const
 
 // x (14, identical on both lanes of the pair), u_own = the own leg's two joint torques.
 // Returns xdot (14) and y (4), identical on both lanes.  mode as wb_dynamics.
-__device__ __forceinline__ void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
+MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
                                                  bool back, real* xdot, real* y) {
+  MHPC_NO_FMA_WB
   const real sg = back ? -real(1.0) : real(1.0);
   // geometry: the body pitch and the own leg's two links
   real sth, cth;

@@ -31,11 +31,11 @@ hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_export(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_reduce_counters(const SolveParams&, const DevBufs&, unsigned long long*,
                                   hipStream_t);
-#ifndef MHPC_FP32
 hipError_t launch_eval_wb_dyn(int, int, const real*, const real*, real*, real*, hipStream_t);
+hipError_t launch_eval_wb_dyn_pair(int, int, const real*, const real*, real*, real*, hipStream_t);
+#ifndef MHPC_FP32
 hipError_t launch_eval_wb_par(int, int, const real*, const real*, real*, real*, real*,
                               real*, hipStream_t);
-hipError_t launch_eval_wb_dyn_pair(int, int, const real*, const real*, real*, real*, hipStream_t);
 hipError_t launch_eval_wb_aux(int, int, const real*, real*, real*, real*, real*, real*, hipStream_t);
 hipError_t launch_eval_wb_impact(int, int, const real*, real*, real*, hipStream_t);
 hipError_t launch_eval_srb(int, const real*, const real*, const real*, const real*,
@@ -876,6 +876,36 @@ extern "C" int mhpc_eval_srb(int device, int n, const double* x, const double* u
   HIPCHK(hipMemcpy(xdot, dxd, n * 6 * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(Ac, dA, n * 36 * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(Bc, dB, n * 24 * sizeof(double), hipMemcpyDeviceToHost));
+  return MHPC_OK;
+}
+#else   // MHPC_FP32: the fp32 build of the two rollout dynamics models
+// Whole-body dynamics of the fp32 instantiation, single-lane (pair = 0: xdot [n][14],
+// y [n][4]) or lane pair (pair = 1: xdot [n][2][14], y [n][2][4]); host arrays double.
+extern "C" int mhpc_eval_wb_dynamics_f32(int device, int n, int mode, int pair, const double* x,
+                                         const double* u, double* xdot, double* y) {
+  if (n < 1 || !x || !u || !xdot || !y || mode < 1 || mode > 4 || (pair != 0 && pair != 1))
+    return fail(MHPC_ERR_INVALID, "bad argument");
+  HIPCHK(hipSetDevice(device));
+  const int L = pair ? 2 : 1;
+  std::vector<float> hx(x, x + (size_t)n * 14), hu(u, u + (size_t)n * 4);
+  std::vector<float> hxd((size_t)n * 14 * L), hy((size_t)n * 4 * L);
+  float *dx = nullptr, *du = nullptr, *dxd = nullptr, *dy = nullptr;
+  hipError_t e = hipMalloc((void**)&dx, hx.size() * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&du, hu.size() * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&dxd, hxd.size() * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&dy, hy.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(dx, hx.data(), hx.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(du, hu.data(), hu.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = pair ? launch_eval_wb_dyn_pair(n, mode, dx, du, dxd, dy, nullptr)
+             : launch_eval_wb_dyn(n, mode, dx, du, dxd, dy, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(hxd.data(), dxd, hxd.size() * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(hy.data(), dy, hy.size() * 4, hipMemcpyDeviceToHost);
+  for (float* p : {dx, du, dxd, dy})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("mhpc_eval_wb_dynamics_f32: ") + hipGetErrorString(e));
+  std::copy(hxd.begin(), hxd.end(), xdot);
+  std::copy(hy.begin(), hy.end(), y);
   return MHPC_OK;
 }
 #endif  // MHPC_FP32

@@ -79,6 +79,23 @@ def test_wb_dynamics_pair_bitwise(kat, L, mode):
         np.testing.assert_array_equal(y2[:, lane], y, err_msg=f"lane {lane} y")
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_wb_dynamics_pair_bitwise_fp32(kat, L, mode):
+    """The same in the fp32 instantiation (C5 fp32 runs both line-search variants too)."""
+    x, u = kat["x"], kat["u"]
+    n = len(x)
+    xd, y = np.zeros((n, 14)), np.zeros((n, 4))
+    L.check(L.lib().mhpc_eval_wb_dynamics_f32(0, n, mode, 0, L.dptr(x), L.dptr(u), L.dptr(xd),
+                                              L.dptr(y)))
+    xd2, y2 = np.zeros((n, 2, 14)), np.zeros((n, 2, 4))
+    L.check(L.lib().mhpc_eval_wb_dynamics_f32(0, n, mode, 1, L.dptr(x), L.dptr(u), L.dptr(xd2),
+                                              L.dptr(y2)))
+    assert np.isfinite(xd).all()
+    for lane in (0, 1):
+        np.testing.assert_array_equal(xd2[:, lane], xd, err_msg=f"lane {lane} xdot")
+        np.testing.assert_array_equal(y2[:, lane], y, err_msg=f"lane {lane} y")
+
+
 @pytest.mark.parametrize("foot,td,jac", [(0, "WB_FL1_terminal_constr", "Jacob_F"),
                                          (1, "WB_FL2_terminal_constr", "Jacob_B")])
 def test_touchdown_and_foot_jacobian(kat, L, foot, td, jac):

@@ -67,7 +67,7 @@ ALL_VARIANTS = list(itertools.product(("1wave", "2wave"),
 def test_variant_rejected_when_it_does_not_apply(need_gpu):
     from mhpc_minimal_env_amd import capi, configs, locomotion as L
     opt = L.HSDDP_OPTION()
-    opt.alpha = 0.3  # 1, 0.3, 0.09, ...: fewer than 10 candidates -> no staged variants
+    opt.alpha = 0.01  # 1, 1e-2, ..., 1e-8: 5 candidates -> no staged / pair variants
     loco = L.MHPCLocomotion(desc=configs.c3_desc(), option=opt, batch=2, device=0)
     try:
         for v in ("pair", "pipe_staged", "fused_staged"):
