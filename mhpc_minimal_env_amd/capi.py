@@ -25,7 +25,7 @@ MHPC_ERR_INVALID = 1
 # mhpc_set_kernel_variant (include/mhpc_capi.h)
 MHPC_VARIANT_BWS = 0
 MHPC_VARIANT_RO = 1
-BWS_VARIANTS = {"auto": 0, "1wave": 1, "2wave": 2}
+BWS_VARIANTS = {"auto": 0, "1wave": 1, "2wave": 2, "pairwave": 3}
 RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged": 4, "fused": 5}
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1

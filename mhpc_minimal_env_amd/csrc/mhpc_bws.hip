@@ -450,9 +450,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
       s += t * sh.Q[(NX + c) * QS + QV];
     }
-    // s and psd are uniform: every lane writes the same value (no divergent branch)
+    // s and psd are uniform: every lane of wave 0 writes the same value (no divergent
+    // branch); the other waves of a 128-thread block must not re-read the updated dV
     const real dv0 = sh.dV;
-    sh.dV = psd ? dv0 + -s : dv0;
+    *(lane < 64 ? &sh.dV : &sh.junk[lane & 63]) = psd ? dv0 + -s : dv0;
   }
   {
     // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
@@ -843,8 +844,10 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     fb_w2 = 2 * dt * cRfb[m][c];
     fb_rx = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
   }
-  const int xo = lane < 10 ? lane : 0;
-  const bool isref = lane == 10;
+  // every wave of the block loads the same nominal words (lane & 63), so the uniform W
+  // entries of the drop below are the same values whichever wave writes them
+  const int xo = (lane & 63) < 10 ? (lane & 63) : 0;
+  const bool isref = (lane & 63) == 10;
   auto loadx = [&](int k) {  // unconditional single load per lane (no exec-masked load)
     const real* tk = traj_ptr(sp, d, b, nom, ko + k);
     return *(isref ? pos + k : tk + xo);
@@ -1010,11 +1013,14 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
   hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s, sp,
                      d, update_reg);
 #else
-  const bool one = sp.var_bws ? sp.var_bws == MHPC_VARIANT_BWS_1WAVE : sp.B <= 4 * sp.ncu;
-  if (one)
+  const int v = sp.var_bws ? sp.var_bws
+                           : sp.B <= 4 * sp.ncu ? MHPC_VARIANT_BWS_1WAVE : MHPC_VARIANT_BWS_2WAVE;
+  if (v == MHPC_VARIANT_BWS_1WAVE)
     hipLaunchKernelGGL((k_bws<64, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else
+  else if (v == MHPC_VARIANT_BWS_2WAVE)
     hipLaunchKernelGGL((k_bws<64, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else
+    hipLaunchKernelGGL((k_bws<128, 2>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
 #endif
   return hipGetLastError();
 }

@@ -60,7 +60,7 @@ def assert_oracle(got, ref, tol=SOLVE_TOL):
         assert err <= tol, (k, err)
 
 
-ALL_VARIANTS = list(itertools.product(("1wave", "2wave"),
+ALL_VARIANTS = list(itertools.product(("1wave", "2wave", "pairwave"),
                                       ("pair", "pipe_staged", "pipe", "fused_staged", "fused")))
 
 
@@ -75,7 +75,7 @@ def test_variant_rejected_when_it_does_not_apply(need_gpu):
                 loco.set_kernel_variant(rollout=v)
         loco.set_kernel_variant(bws="2wave", rollout="fused")
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 7, 0) == capi.MHPC_ERR_INVALID
-        assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 3) == capi.MHPC_ERR_INVALID
+        assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 4) == capi.MHPC_ERR_INVALID
     finally:
         loco.close()
 
