@@ -197,12 +197,12 @@ def workload_text(name: str) -> str:
 class Solver:
     """One handle on this rank's GPU, stepping init + solve of its batch."""
 
-    def __init__(self, desc, opt, x0, device, variants=("auto", "auto")):
+    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto")):
         from mhpc_minimal_env_amd import capi
         from mhpc_minimal_env_amd import locomotion as L
         self.capi = capi
         self.loco = L.MHPCLocomotion(desc=desc, option=opt, batch=x0.shape[0], device=device)
-        self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1])
+        self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2])
         self.loco.set_initial_condition(x0)
         self.lib, self.h = capi.lib(), self.loco._h
         capi.check(self.lib.mhpc_set_x0(self.h, capi.dptr(self.loco._x0)), "mhpc_set_x0")
@@ -305,7 +305,7 @@ def run_sweep(args, torch):
     from mhpc_minimal_env_amd import configs
     desc, opt = workload(args.workload)
     for B in [int(b) for b in args.batch_sweep.split(",")]:
-        s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant))
+        s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant, args.overlap))
         for _ in range(args.warmup):
             s.step()
         s.loco.set_profiling(True)
@@ -363,6 +363,8 @@ def main():
                     help="pin the backward-sweep launch variant (capi.BWS_VARIANTS; tuning only)")
     ap.add_argument("--ro-variant", default="auto",
                     help="pin the line-search launch variant (capi.RO_VARIANTS; tuning only)")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="partials beside the SRB half of the backward sweep (tuning only)")
     ap.add_argument("--batch-sweep", default=None,
                     help="comma-separated batch sizes: one JSON line each (1 GPU)")
     args = ap.parse_args()
@@ -403,7 +405,7 @@ def main():
     x0 = configs.x0_for(desc, B, offset=rank * B)
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
-    s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant))
+    s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant, args.overlap))
     for _ in range(args.warmup):
         s.step()
     s.loco.set_profiling(True)

@@ -199,6 +199,10 @@ void mhpc_destroy(mhpc_handle* h);
 #define MHPC_VARIANT_RO_PIPE 3        /*   two-wave pipeline, operands from HBM */
 #define MHPC_VARIANT_RO_FUSED_STAGED 4 /*  one wave, LDS-staged operands */
 #define MHPC_VARIANT_RO_FUSED 5       /*   one wave, operands from HBM */
+#define MHPC_VARIANT_OVERLAP 2        /* which: partials beside the SRB half of the sweep */
+#define MHPC_VARIANT_OVERLAP_ON 1     /*   two launches + second stream (default when both
+                                         WB and SRB phases are present) */
+#define MHPC_VARIANT_OVERLAP_OFF 2    /*   one sweep launch after the partials */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

@@ -905,21 +905,42 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
   return true;
 }
 
-template <int NT>
+// One sweep attempt with regularisation reg.  PART 0: every phase, from a zero terminal
+// value function (MultiPhaseDDP::backward_sweep).  PART 1: only the SRB phases (P-1 ..
+// n_wb), which read no partials record, so this launch can run beside the partials of the
+// same iteration.  PART 2: the WB phases (n_wb-1 .. 0), resuming from the value function
+// PART 1 left in d.carry.  PART 1 then PART 2 is PART 0's arithmetic, bit for bit (the
+// carried H / G / dV are stored and reloaded exactly).
+template <int NT, int PART>
 __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st, BwsLds& sh,
-                          real reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads) {
+                          real reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads,
+                          bool from_carry = true) {
   const int lane = threadIdx.x;
   const int nom = st->nom_slot;
-  #pragma unroll 1
-  for (int e = lane; e < 196; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
-  if (lane < 14) sh.G[lane] = 0;
-  if (lane == 0) sh.dV = 0;
+  if (PART == 2) {
+    // resume: the value function from d.carry, or as a PART 1 sweep of this kernel left it
+    const BwsCarry& c = d.carry[b];
+    if (from_carry) {
+      #pragma unroll 1
+      for (int e = lane; e < 196; e += NT) sh.H[e] = c.H[e];
+      if (lane < 14) sh.G[lane] = c.G[lane];
+    }
+  } else {
+    #pragma unroll 1
+    for (int e = lane; e < 196; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
+    if (lane < 14) sh.G[lane] = 0;
+    if (lane == 0) sh.dV = 0;
+  }
   __syncthreads();
-  for (int p = sp.P - 1; p >= 0; --p) {
-    const bool wb = p < sp.n_wb;
+  const int p_hi = PART == 2 ? sp.n_wb - 1 : sp.P - 1;
+  const int p_lo = PART == 1 ? sp.n_wb : 0;
+  for (int p = p_hi; p >= p_lo; --p) {
+    const bool wb = PART == 1 ? false : p < sp.n_wb;
     const int N = sp.N[p], ko = sp.ko[p];
     if (p + 1 < sp.P) {
-      if (wb) impact_step<NT>(sp, d, b, sh, lane, p, px_reads);
+      if constexpr (PART != 1) {
+        if (wb) impact_step<NT>(sp, d, b, sh, lane, p, px_reads);
+      }
       if (lane == 0) sh.dV = st->dV[p + 1];  // dVnext
     }
     __syncthreads();
@@ -928,13 +949,16 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
     const real* xe = traj_ptr(sp, d, b, nom, ko + N - 1);
     int64_t kn = 0;
     bool ok;
-    if (wb) {
-      terminal_value<NT, 14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
-      const int mode = sp.mode[p];
-      ok = (mode == 1 || mode == 3) ? sweep_wb_phase<NT, true>(sp, d, b, st, sh, lane, p, reg, &kn)
-                                    : sweep_wb_phase<NT, false>(sp, d, b, st, sh, lane, p, reg, &kn);
-      *knots_wb += kn;
-    } else {
+    if constexpr (PART != 1) {
+      if (wb) {
+        terminal_value<NT, 14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
+        const int mode = sp.mode[p];
+        ok = (mode == 1 || mode == 3) ? sweep_wb_phase<NT, true>(sp, d, b, st, sh, lane, p, reg, &kn)
+                                      : sweep_wb_phase<NT, false>(sp, d, b, st, sh, lane, p, reg, &kn);
+        *knots_wb += kn;
+      }
+    }
+    if (!wb) {
       terminal_value<NT, 6>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
       ok = sweep_fb_phase<NT>(sp, d, b, st, sh, lane, p, reg, &kn);
     }
@@ -951,7 +975,12 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
 // per problem; while the batch fits one wave per SIMD (B <= 4 x CUs) the 1-wave build (no
 // register cap, widest ILP) is fastest, beyond that the 2-wave build hides latency by
 // co-residency.
-template <int NT, int WAVES>
+//
+// PART 0: the whole sweep with its regularisation retries (MultiPhaseDDP.cpp:196-241).
+// PART 1: the SRB phases of the first attempt only, the value function at the WB boundary
+// saved to d.carry.  PART 2: the WB phases of the first attempt (if PART 1 passed), then the
+// same retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
+template <int NT, int WAVES, int PART>
 __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, real update_reg) {
   const int b = blockIdx.x;
   if (b >= sp.B) return;
@@ -962,18 +991,48 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
   int bws_iter = 1;
   int64_t knots = 0, knots_wb = 0, px_reads = 0, sweeps = 0;
   bool aborted = false;
+  if constexpr (PART == 1) {
+    const bool ok = bws_sweep<NT, 1>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
+    BwsCarry& c = d.carry[b];
+    #pragma unroll 1
+    for (int e = threadIdx.x; e < 196; e += NT) c.H[e] = sh.H[e];
+    if (threadIdx.x < 14) c.G[threadIdx.x] = sh.G[threadIdx.x];
+    if (threadIdx.x == 0) {
+      c.ok = ok ? 1 : 0;
+      c.knots = (int32_t)knots;
+    }
+    return;
+  }
+  if constexpr (PART == 2) {
+    // PART 0's loop below, the SRB half of its first attempt taken from PART 1; every
+    // retry runs both halves here (one call site each: the WB sweep code exists once)
+    const BwsCarry& c = d.carry[b];
+    knots = c.knots;
+    for (bool first = true;; first = false) {
+      ++sweeps;
+      bool ok = first ? c.ok != 0
+                      : bws_sweep<NT, 1>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
+      if (ok) ok = bws_sweep<NT, 2>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads, first);
+      if (ok) break;
+      reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
+      ++bws_iter;
+      if (reg > 1000) { aborted = true; break; }
+    }
+  }
 #ifdef MHPC_BWS_TIMING
   if (threadIdx.x < 12) sh.cyc[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh.tlast = clock64();
   const unsigned long long t_start = clock64();
   __syncthreads();
 #endif
-  for (;;) {
-    ++sweeps;
-    if (bws_sweep<NT>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
-    reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
-    ++bws_iter;
-    if (reg > 1000) { aborted = true; break; }
+  if constexpr (PART == 0) {
+    for (;;) {
+      ++sweeps;
+      if (bws_sweep<NT, 0>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
+      reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
+      ++bws_iter;
+      if (reg > 1000) { aborted = true; break; }
+    }
   }
   __syncthreads();
 #ifdef MHPC_BWS_TIMING
@@ -1008,21 +1067,39 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
 // Variant: sp.var_bws (mhpc_set_kernel_variant) or, by default, the 1-wave build while the
 // batch fits one wave per SIMD of the handle's device (sp.ncu), the 2-wave build beyond.
 // Both builds compile the same source; tests/test_gpu_variants.py checks them bit for bit.
-hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, hipStream_t s) {
+// part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).  The SRB half reads no
+// partials record and needs few registers (the WB code is not instantiated), so a partials
+// wave fits beside it on a SIMD.
+hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, int part,
+                      hipStream_t s) {
 #ifdef MHPC_BWS_WAVES
-  hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s, sp,
-                     d, update_reg);
+  hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES, 0>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s,
+                     sp, d, update_reg);
+  (void)part;
 #else
   const int v = sp.var_bws ? sp.var_bws
                            : sp.B <= 4 * sp.ncu ? MHPC_VARIANT_BWS_1WAVE : MHPC_VARIANT_BWS_2WAVE;
-  if (v == MHPC_VARIANT_BWS_1WAVE)
-    hipLaunchKernelGGL((k_bws<64, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  if (part == 1)
+    hipLaunchKernelGGL((k_bws<64, 2, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else if (v == MHPC_VARIANT_BWS_1WAVE && part == 2)
+    hipLaunchKernelGGL((k_bws<64, 1, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else if (v == MHPC_VARIANT_BWS_2WAVE && part == 2)
+    hipLaunchKernelGGL((k_bws<64, 2, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else if (v == MHPC_VARIANT_BWS_1WAVE)
+    hipLaunchKernelGGL((k_bws<64, 1, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_2WAVE)
-    hipLaunchKernelGGL((k_bws<64, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<64, 2, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else
-    hipLaunchKernelGGL((k_bws<128, 2>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<128, 2, 0>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
 #endif
   return hipGetLastError();
+}
+
+// Whether the sweep runs as an SRB launch beside the partials and a WB launch after them:
+// both kinds of phase present, the 64-thread builds, not switched off (var_overlap 2).
+bool bws_split(const SolveParams& sp) {
+  return sp.n_wb > 0 && sp.P > sp.n_wb && sp.var_overlap != 2 &&
+         sp.var_bws != MHPC_VARIANT_BWS_PAIRWAVE;
 }
 
 }  // namespace MHPC_NS

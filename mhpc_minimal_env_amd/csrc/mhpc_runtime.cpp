@@ -16,7 +16,8 @@ namespace MHPC_NS {
 hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
-hipError_t launch_bws(const SolveParams&, const DevBufs&, real, hipStream_t);
+hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
+bool bws_split(const SolveParams&);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_zero_tails(const SolveParams&, const DevBufs&, hipStream_t);
@@ -75,6 +76,10 @@ struct Handle {
   SolveParams sp;
   DevBufs d;
   hipStream_t stream = nullptr;
+  // second stream: the partials run there beside the SRB half of the backward sweep
+  // (fork / join events order it against the main stream)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t evfork = nullptr, evjoin = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool x0_set = false, initialized = false, solved = false, x0_changed = false;
   float solve_ms = 0;
@@ -197,7 +202,7 @@ static int validate(const mhpc_problem_desc* d) {
 
 static void free_bufs(Handle* h) {
   DevBufs& d = h->d;
-  void* ptrs[] = {d.traj, d.refpos, d.K, d.du, d.G, d.par, d.px, d.x0, d.st, d.out};
+  void* ptrs[] = {d.traj, d.refpos, d.K, d.du, d.G, d.par, d.px, d.x0, d.st, d.out, d.carry};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   memset(&d, 0, sizeof d);
@@ -270,12 +275,16 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   alloc((void**)&d.x0, B * 14 * sizeof(real));
   alloc((void**)&d.st, B * sizeof(ProbState));
   alloc((void**)&d.out, B * NK * KS * sizeof(real));
+  alloc((void**)&d.carry, B * sizeof(BwsCarry));
   alloc((void**)&h->dcnt, NCNT * sizeof(unsigned long long));
   h->nk_cap = sp.NK;
   h->nbk = kPhaseBufKnots;
   for (int p = 0; p < sp.P; ++p) h->nbk = std::max(h->nbk, sp.N[p]);
   alloc((void**)&h->store, B * sp.P * (size_t)h->nbk * kStoreRec * sizeof(real));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evfork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evjoin, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
   // zero x0 on the handle's own (non-blocking) stream: a null-stream memset would not be
@@ -311,23 +320,25 @@ int api_set_x0(Handle* h, const double* x0) {
   return MHPC_OK;
 }
 
-static int mark(Handle* h, int kind) {
+static int mark(Handle* h, int kind, hipStream_t s) {
   if (!h->profile) return MHPC_OK;
   hipEvent_t e;
   HIPCHK(hipEventCreate(&e));
-  HIPCHK(hipEventRecord(e, h->stream));
+  HIPCHK(hipEventRecord(e, s));
   h->evpool.push_back(e);
   h->evkind.push_back(kind);
   return MHPC_OK;
 }
-#define LAUNCH(h, kind, expr)          \
+// one launch on stream s, bracketed by profiling events on the same stream
+#define LAUNCH_ON(h, kind, s, expr)    \
   do {                                 \
-    int rc_ = mark(h, kind);           \
+    int rc_ = mark(h, kind, s);        \
     if (rc_) return rc_;               \
     HIPCHK(expr);                      \
-    rc_ = mark(h, -1);                 \
+    rc_ = mark(h, -1, s);              \
     if (rc_) return rc_;               \
   } while (0)
+#define LAUNCH(h, kind, expr) LAUNCH_ON(h, kind, h->stream, expr)
 
 static int collect_profile(Handle* h) {
   for (size_t i = 0; i + 1 < h->evpool.size(); i += 2) {
@@ -395,10 +406,35 @@ int api_initialize(Handle* h) {
 
 // MultiPhaseDDP::solve (MultiPhaseDDP.cpp:154-289) as a fixed launch schedule; every kernel
 // skips the problems whose device state machine has left the corresponding loop.
+// With bws_split the partials of an iteration run on the second stream beside the SRB half
+// of the backward sweep (which reads no partials record); the WB half waits for them.
 static int solve_async(Handle* h) {
   const SolveParams& sp = h->sp;
   const DevBufs& d = h->d;
   const mhpc_hsddp_option& o = h->opt;
+  const bool split = bws_split(sp);
+  auto partials = [&]() -> int {
+    if (!split) {
+      LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
+      return MHPC_OK;
+    }
+    HIPCHK(hipEventRecord(h->evfork, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->stream2, h->evfork, 0));
+    LAUNCH_ON(h, K_PAR, h->stream2, launch_partials(sp, d, h->stream2));
+    HIPCHK(hipEventRecord(h->evjoin, h->stream2));
+    return MHPC_OK;
+  };
+  auto bws = [&]() -> int {
+    if (!split) {
+      LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 0, h->stream));
+      return MHPC_OK;
+    }
+    LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 1, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
+    LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 2, h->stream));
+    return MHPC_OK;
+  };
+  int rc;
   int n_al = 0;
   for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
   for (int al = 1; al <= o.max_AL_iter; ++al) {
@@ -406,13 +442,13 @@ static int solve_async(Handle* h) {
       LAUNCH(h, K_FULL, launch_rollout(sp, d, al, 0, 0, 1, h->stream));
     else
       LAUNCH(h, K_FULL, launch_cost(sp, d, al, h->stream));  // forward_sweep(0)
-    LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
+    if ((rc = partials())) return rc;
     int max_ddp = 0;
     for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
     for (int ddp = 1; ddp <= max_ddp; ++ddp) {
-      LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, h->stream));
+      if ((rc = bws())) return rc;
       LAUNCH(h, K_LS, launch_rollout(sp, d, al, ddp, max_ddp, 0, h->stream));  // forward_iteration
-      if (ddp < max_ddp) LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
+      if (ddp < max_ddp && (rc = partials())) return rc;
     }
     LAUNCH(h, K_AL, launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
   }
@@ -715,6 +751,11 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
     sp.var_bws = variant;
     return MHPC_OK;
   }
+  if (which == MHPC_VARIANT_OVERLAP) {
+    if (variant < 0 || variant > MHPC_VARIANT_OVERLAP_OFF) return fail(MHPC_ERR_INVALID, "no such overlap variant");
+    sp.var_overlap = variant;
+    return MHPC_OK;
+  }
   if (which != MHPC_VARIANT_RO) return fail(MHPC_ERR_INVALID, "no such kernel");
   if (variant < 0 || variant > MHPC_VARIANT_RO_FUSED) return fail(MHPC_ERR_INVALID, "no such line-search variant");
   const bool staged = variant == MHPC_VARIANT_RO_PAIR || variant == MHPC_VARIANT_RO_PIPE_STAGED ||
@@ -751,6 +792,10 @@ void api_destroy(Handle* h) {
   for (hipEvent_t e : h->evpool) (void)hipEventDestroy(e);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->evfork) (void)hipEventDestroy(h->evfork);
+  if (h->evjoin) (void)hipEventDestroy(h->evjoin);
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }

@@ -61,7 +61,7 @@ struct SolveParams {
   int par_item_off[MAXP + 1], par_v_off[MAXP + 1];
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
-  int ncu, var_bws, var_ro;
+  int ncu, var_bws, var_ro, var_overlap;
 };
 
 struct ProbState {
@@ -98,6 +98,16 @@ struct ProbState {
   real opt_pen, cap_pen;
 };
 
+// Value function where the backward sweep crosses from the SRB phases into the WB phases
+// (the sweep runs as two launches when the SRB part overlaps the partials):
+// H / G of knot 0 of phase n_wb (row stride NX of that phase), whether that part of the
+// first sweep attempt passed the PSD test, and the knots it swept.
+struct BwsCarry {
+  real H[196];
+  real G[14];
+  int32_t ok, knots;
+};
+
 struct DevBufs {
   real* traj;
   real* refpos;
@@ -109,6 +119,7 @@ struct DevBufs {
   real* x0;
   ProbState* st;
   real* out;    // export staging [B][NK][KS]
+  BwsCarry* carry;  // [B]
 };
 
 // ---- cost weights (MHPCCost.cpp:24-75) and constraint constants (MHPCConstraints.cpp) --

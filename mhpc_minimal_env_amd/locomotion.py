@@ -343,10 +343,13 @@ class MHPCLocomotion:
     def reset_kernel_stats(self):
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
-    def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto"):
-        """Pin the backward-sweep / line-search launch variant (mhpc_set_kernel_variant);
-        names in capi.BWS_VARIANTS / capi.RO_VARIANTS, "auto" = chosen by batch size."""
+    def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto"):
+        """Pin the backward-sweep / line-search launch variant and the partials / sweep
+        overlap (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
+        capi.OVERLAP_VARIANTS, "auto" = chosen by batch size and phase layout."""
         L = capi.lib()
+        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_OVERLAP,
+                                             capi.OVERLAP_VARIANTS[overlap]), "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_BWS,
                                              capi.BWS_VARIANTS[bws]), "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO,

@@ -28,11 +28,11 @@ def _oracle():
     return O if O.available() else None
 
 
-def solve(desc, x0, bws="auto", rollout="auto", rows=None):
+def solve(desc, x0, bws="auto", rollout="auto", rows=None, overlap="auto"):
     from mhpc_minimal_env_amd import locomotion as L
     loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=x0.shape[0], device=0)
     try:
-        loco.set_kernel_variant(bws=bws, rollout=rollout)
+        loco.set_kernel_variant(bws=bws, rollout=rollout, overlap=overlap)
         loco.set_initial_condition(x0)
         loco.initialization()
         status = loco.solve_mhpc().copy()
@@ -60,8 +60,12 @@ def assert_oracle(got, ref, tol=SOLVE_TOL):
         assert err <= tol, (k, err)
 
 
-ALL_VARIANTS = list(itertools.product(("1wave", "2wave", "pairwave"),
-                                      ("pair", "pipe_staged", "pipe", "fused_staged", "fused")))
+ALL_VARIANTS = [(b, r, "auto") for b, r in
+                itertools.product(("1wave", "2wave", "pairwave"),
+                                  ("pair", "pipe_staged", "pipe", "fused_staged", "fused"))]
+# the backward sweep as one launch after the partials (the default splits it into an SRB
+# launch beside the partials and a WB launch after them)
+ALL_VARIANTS += [("1wave", "pair", "off"), ("2wave", "fused", "off"), ("auto", "auto", "off")]
 
 
 def test_variant_rejected_when_it_does_not_apply(need_gpu):
@@ -75,6 +79,7 @@ def test_variant_rejected_when_it_does_not_apply(need_gpu):
                 loco.set_kernel_variant(rollout=v)
         loco.set_kernel_variant(bws="2wave", rollout="fused")
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 7, 0) == capi.MHPC_ERR_INVALID
+        assert capi.lib().mhpc_set_kernel_variant(loco._h, 2, 3) == capi.MHPC_ERR_INVALID
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 4) == capi.MHPC_ERR_INVALID
     finally:
         loco.close()
@@ -88,8 +93,9 @@ def test_c3_every_variant_bitwise_and_vs_oracle(need_gpu):
     O = _oracle()
     if O is not None:
         assert_oracle(base, O.solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=8))
-    for bws, ro in ALL_VARIANTS:
-        assert_bitwise(solve(desc, x0, bws, ro), base, f"C3 bws={bws} rollout={ro}")
+    for bws, ro, ov in ALL_VARIANTS:
+        assert_bitwise(solve(desc, x0, bws, ro, overlap=ov), base,
+                       f"C3 bws={bws} rollout={ro} overlap={ov}")
 
 
 @pytest.mark.parametrize("precision", [64, 32])
@@ -100,8 +106,9 @@ def test_c5_every_variant_bitwise(need_gpu, precision):
     base = solve(desc, x0)
     if precision == 64 and _oracle() is not None:
         assert_oracle(base, _oracle().solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=8))
-    for bws, ro in ALL_VARIANTS:
-        assert_bitwise(solve(desc, x0, bws, ro), base, f"C5/{precision} bws={bws} rollout={ro}")
+    for bws, ro, ov in ALL_VARIANTS:
+        assert_bitwise(solve(desc, x0, bws, ro, overlap=ov), base,
+                       f"C5/{precision} bws={bws} rollout={ro} overlap={ov}")
 
 
 def _sample(B, n=64):
