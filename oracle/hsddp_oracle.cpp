@@ -882,6 +882,9 @@ void mp_solve(Problem& P) {
     if (P.tconstr_violation < P.opt.AL_thresh) break;
     iter_AL++;
   }
+  // the boundary's status extension (include/mhpc_capi.h; the reference returns nothing):
+  // a solve that ran to the end with a non-finite total cost
+  if (P.status == MHPC_SOLVE_OK && !std::isfinite(P.actual_cost)) P.status = MHPC_SOLVE_NONFINITE;
 }
 
 // ---- problem construction (MHPCLocomotion::build_problem, ReferenceGen, warmstart) -----

@@ -90,8 +90,26 @@ def make_solve(name):
     return res
 
 
+def make_edge(name):
+    """Solves that reach the rare branches (tests/_edge_cases.py): inputs + oracle outputs."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import _edge_cases as E
+    desc, opt, x0 = E.inputs(name)
+    res = O.solve(desc, opt.to_c(), x0, nthreads=4)
+    # per-problem scalars and decision traces only (the trajectories of 64 problems would be
+    # megabytes; the GPU tests compare those against the live oracle)
+    keep = {k: res[k] for k in ("J", "dV_exp", "viol", "V", "dV", "status", "trace", "counters")}
+    keep["x0"] = x0
+    keep["desc"] = np.array(str(desc.describe()))
+    return keep
+
+
 def main():
     assert O.available(), "build the oracle and oracle/_ref first (make -C oracle)"
+    sys.path.insert(0, os.path.dirname(HERE))
+    import _edge_cases as E
+    for name in E.CASES:
+        np.savez_compressed(os.path.join(HERE, f"edge_{name}.npz"), **make_edge(name))
     np.savez_compressed(os.path.join(HERE, "kat_model.npz"), **make_kat())
     for name in SOLVES:
         np.savez_compressed(os.path.join(HERE, f"solve_{name}.npz"), **make_solve(name))
