@@ -1082,6 +1082,51 @@ void export_problem(const Problem& P, int b, const mhpc_problem_desc* d, double*
 
 }  // namespace
 
+// One knot of SinglePhase::backward_sweep (SinglePhase.cpp:197-212) on caller-supplied
+// blocks, exactly the body of phase_backward_sweep: compute_Qfunction, + reg on the Qxx / Quu
+// diagonals, the PSD test of Quu - 1e-9 I, valuefunction_update.  Row-major A [n][n],
+// B [n][4], C [4][n], D [4][4], lxx [n][n], lux [4][n], luu / lyy [4][4], Hn [n][n].
+// Returns 1 (PSD, K / du / G / H / dV written) or 0 (not PSD, nothing written); tests only.
+extern "C" int oracle_riccati_knot(int n, const double* A, const double* B, const double* C,
+                                   const double* D, const double* lx, const double* lu,
+                                   const double* ly, const double* lxx, const double* lux,
+                                   const double* luu, const double* lyy, const double* Gn,
+                                   const double* Hn, double reg, double* K, double* du,
+                                   double* G, double* H, double* dV) {
+  if (n < 1 || n > 14) return -1;
+  Par p{};
+  RCost rc{};
+  CTG c{};
+  memcpy(p.A, A, sizeof(double) * n * n);
+  memcpy(p.B, B, sizeof(double) * n * 4);
+  memcpy(p.C, C, sizeof(double) * 4 * n);
+  memcpy(p.D, D, sizeof(double) * 16);
+  memcpy(rc.lx, lx, sizeof(double) * n);
+  memcpy(rc.lu, lu, sizeof(double) * 4);
+  memcpy(rc.ly, ly, sizeof(double) * 4);
+  memcpy(rc.lxx, lxx, sizeof(double) * n * n);
+  memcpy(rc.lux, lux, sizeof(double) * 4 * n);
+  memcpy(rc.luu, luu, sizeof(double) * 16);
+  memcpy(rc.lyy, lyy, sizeof(double) * 16);
+  compute_Qfunction(c, rc, p, Gn, Hn, n);
+  for (int i = 0; i < n; ++i) c.Qxx[i * n + i] += 1.0 * reg;
+  for (int i = 0; i < 4; ++i) c.Quu[i * 4 + i] += 1.0 * reg;
+  double Qr[16];
+  const double eps9 = pow(0.1, 9);
+  for (int i = 0; i < 16; ++i) Qr[i] = c.Quu[i] - ((i % 5 == 0) ? 1.0 * eps9 : 0.0);
+  if (!ldlt_is_positive(Qr, 4)) return 0;
+  const double d = valuefunction_update(c, n);
+  memcpy(K, c.K, sizeof(double) * 4 * n);
+  memcpy(du, c.du, sizeof(double) * 4);
+  memcpy(G, c.G, sizeof(double) * n);
+  memcpy(H, c.H, sizeof(double) * n * n);
+  *dV = d;
+  return 1;
+}
+
+// Eigen::LDLT(A).isPositive() as the oracle restates it (row-major 4x4); tests only.
+extern "C" int oracle_ldlt_is_positive(const double* A) { return ldlt_is_positive(A, 4) ? 1 : 0; }
+
 extern "C" int oracle_load_ref(const char* path) {
   if (g_ref.handle) return 0;
   g_ref.handle = dlopen(path, RTLD_NOW | RTLD_LOCAL);

@@ -21,7 +21,7 @@ def test_c5_fp32_vs_fp64_oracle(need_gpu):
     if not O.available():
         pytest.skip("oracle not built")
     from mhpc_minimal_env_amd import configs, locomotion as L
-    B = 32
+    B = 64
     desc32 = configs.c5f32_desc()
     x0 = configs.x0_for(desc32, B)
     loco = L.MHPCLocomotion(desc=desc32, option=L.HSDDP_OPTION(), batch=B, device=0)
