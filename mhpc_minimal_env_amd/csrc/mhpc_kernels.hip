@@ -881,9 +881,9 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
 // warm = 0 (mhpc_update_problem): references and per-problem state only -- the reference's
 // update_problem() regenerates the references and re-initialises the AL / ReB parameters of
 // every phase but keeps the (rotated) nominal trajectories and gains as the warm start.
-__global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= sp.B) return;
+// References (ReferenceGen.h:94-109) and the per-problem solver state of one problem;
+// warm = 1 also resets the option fields a solve rewrites (see ProbState).
+__device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int warm) {
   const real* x0 = d.x0 + (size_t)b * 14;
   real* pos = d.refpos + (size_t)b * sp.NK;
   for (int p = 0; p < sp.P; ++p) {
@@ -920,6 +920,21 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   st->opt_pen = sp.update_penalty;
   st->cap_reb = st->opt_reb;
   st->cap_pen = st->opt_pen;
+}
+
+// A lane pair per problem (even lane: front leg, odd: back leg of the pair dynamics,
+// mhpc_model_pair.h): the warm-start rollout is one serial chain per problem, so halving its
+// per-knot latency is what counts; both lanes carry the same state and controls (the pair
+// model returns xdot and y on both, bit for bit the single-lane model's), the even lane
+// writes the references and the per-problem state, each lane half of every knot record.
+__global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = t >> 1;
+  const bool back = (t & 1) != 0;
+  if (b >= sp.B) return;  // both lanes of a pair
+  const real* x0 = d.x0 + (size_t)b * 14;
+  if (!back) k_init_state(sp, d, b, warm);
+  if (!warm) return;
   // warm start of the WB phases into slot 0 (bounding_PDcontrol, boundingPDControl.cpp:3-46)
   real x[14];
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
@@ -942,15 +957,20 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
       } else {
         for (int i = 0; i < 4; ++i) u[i] = Kp[i] * (qnom[i] - x[3 + i]) - x[10 + i];
       }
+      const real u2[2] = {back ? u[2] : u[0], back ? u[3] : u[1]};
       real xd[14], y[4];
-      wb_dynamics<real>(x, u, mode, xd, y);
-      real* o = traj_ptr(sp, d, b, 0, ko + k);
-      for (int i = 0; i < 14; ++i) o[i] = x[i];
-      for (int i = 0; i < 4; ++i) { o[14 + i] = u[i]; o[18 + i] = y[i]; }
+      wb_dynamics_pair(x, u2, mode, back, xd, y);
+      // record x (14) u (4) y (4): even lane entries 0..10, odd lane 11..21
+      real rec[22];
+      for (int i = 0; i < 14; ++i) rec[i] = x[i];
+      for (int i = 0; i < 4; ++i) { rec[14 + i] = u[i]; rec[18 + i] = y[i]; }
+      real* o = traj_ptr(sp, d, b, 0, ko + k) + (back ? 11 : 0);
+#pragma unroll
+      for (int i = 0; i < 11; ++i) o[i] = back ? rec[11 + i] : rec[i];
       for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
     }
     real* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
-    for (int i = 0; i < 14; ++i) oe[i] = x[i];
+    if (!back) for (int i = 0; i < 14; ++i) oe[i] = x[i];
     // phase transition exactly as the forward sweep does it (MultiPhaseDDP.cpp:351-379)
     if (p + 1 < sp.P) {
       if (mode == 2 || mode == 4) {
@@ -967,6 +987,7 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   // SRB phases: the reference's first forward_sweep(0) rolls them out with the initial
   // (zero) controls and zero gains -- u = (0 + 0*0) + sum 0*(x - 0) = +0 exactly -- so the
   // nominal is completed here and forward_sweep(0) reduces to a cost evaluation (k_cost).
+  // Both lanes run the (cheap) SRB chain; each writes half of every record.
   if (sp.n_wb == 0)
     for (int i = 0; i < 6; ++i) x[i] = x0[i];
   for (int p = sp.n_wb; p < sp.P; ++p) {
@@ -979,13 +1000,16 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
     for (int k = 0; k < N - 1; ++k) {
       real xd[6];
       srb_dynamics(x, u, f, s, xd);
-      real* o = traj_ptr(sp, d, b, 0, ko + k);
-      for (int i = 0; i < 6; ++i) o[i] = x[i];
-      for (int i = 0; i < 4; ++i) { o[6 + i] = u[i]; o[10 + i] = real(0.0); }
+      real rec[14];
+      for (int i = 0; i < 6; ++i) rec[i] = x[i];
+      for (int i = 0; i < 4; ++i) { rec[6 + i] = u[i]; rec[10 + i] = real(0.0); }
+      real* o = traj_ptr(sp, d, b, 0, ko + k) + (back ? 7 : 0);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) o[i] = back ? rec[7 + i] : rec[i];
       for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
     }
     real* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
-    for (int i = 0; i < 6; ++i) oe[i] = x[i];
+    if (!back) for (int i = 0; i < 6; ++i) oe[i] = x[i];
   }
 }
 
@@ -1227,11 +1251,11 @@ hipError_t launch_zero_tails(const SolveParams& sp, const DevBufs& d, hipStream_
 }
 
 hipError_t launch_reset(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
+  hipLaunchKernelGGL(k_init, dim3((2 * sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
   return hipGetLastError();
 }
 hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, 1);
+  hipLaunchKernelGGL(k_init, dim3((2 * sp.B + 63) / 64), dim3(64), 0, s, sp, d, 1);
   return hipGetLastError();
 }
 hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hipStream_t s) {

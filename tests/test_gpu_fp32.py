@@ -8,12 +8,14 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# Measured on MI355X (32 problems): trace identical for 32/32, relative cost error median
-# 4.3e-5, max 2.0e-3; 64 problems: max 8.7e-3 (the AL x DDP iterations amplify fp32
-# round-off in a few problems).
-FP32_TRACE_MIN = 0.5      # at least half of the problems take the fp64 decisions
-FP32_J_TOL = 5e-2         # relative cost error of those problems, worst case
-FP32_J_MEDIAN_TOL = 1e-3  # ... and typical
+# Measured on MI355X (64 problems; fp32 sweep contracted without the SLP vectoriser,
+# mhpc_minimal_env_amd/csrc/Makefile): trace identical for 64/64, relative cost error median
+# 3.4e-5, max 6.2e-3; the 64-problem sample of the batch-4096 test (test_gpu_variants.py):
+# traces 63/64, max 1.0e-2.  The worst problems' error sits in one WB phase's value (the
+# touchdown AL term amplifies fp32 round-off over the AL x DDP iterations).
+FP32_TRACE_MIN = 0.9      # problems that take the fp64 decisions
+FP32_J_TOL = 2e-2         # relative cost error of those problems, worst case
+FP32_J_MEDIAN_TOL = 1e-4  # ... and typical
 
 
 def test_c5_fp32_vs_fp64_oracle(need_gpu):

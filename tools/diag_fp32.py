@@ -26,3 +26,9 @@ for prec in (64, 32):
     print(f"precision {prec}: status {np.bincount(st)}, trace identical {same.mean():.3f}, "
           f"J rel err median {np.median(rel):.2e} max {rel.max():.2e} "
           f"(same-trace max {rel[same].max() if same.any() else float('nan'):.2e}), finite {np.isfinite(sc['J']).all()}")
+    if prec == 32:
+        w = np.argsort(-rel)[:4]
+        for i in w:
+            print(f"  problem {i}: J fp32 {sc['J'][i]:.6g} oracle {ref['J'][i]:.6g} viol {sc['viol'][i]:.3g}/{ref['viol'][i]:.3g}")
+            print("    V fp32  ", np.array2string(sc["V"][i], precision=4))
+            print("    V oracle", np.array2string(ref["V"][i], precision=4))
