@@ -29,6 +29,12 @@ namespace MHPC_NS {
 constexpr int WS = 24;          // row stride of W / G2 (columns of [A B], padded)
 constexpr int JR = 24;          // rows of Jt (padded)
 constexpr int QR = 24;          // rows of Q (padded)
+// Row stride of Jt: NX + 1 puts the rows a half-wave reads together in R3 on distinct LDS
+// banks (stride NX = 14 doubles maps rows 16, 17 onto the banks of rows 0, 1).
+#ifndef MHPC_BWS_JTPAD
+#define MHPC_BWS_JTPAD 1
+#endif
+template <int NX> constexpr int JtStride = NX + MHPC_BWS_JTPAD;
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
   static constexpr int QS = NX == 14 ? 22 : 13;  // row stride of Q; column QV holds Qv
@@ -45,7 +51,7 @@ struct BwsLds {
   real lyy2[4], ly2[2];
   union {
     struct {
-      real Jt[JR * 14];  // [A B]' H   (NR x NX)
+      real Jt[JR * 15];  // [A B]' H   (NR x NX, row stride JtStride<NX>)
       real Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
     };
     struct {
@@ -307,7 +313,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int u = 0; u < C; ++u) {
         if (t0 + u >= T2) continue;
         const int row = g + GR * (t0 + u);
-        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * NX + j];
+        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * JtStride<NX> + j];
         *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
       }
     }
@@ -326,7 +332,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const bool wr = g < RG;
     real jr[NQ];
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * NX + NQ + r];
+    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * JtStride<NX> + NQ + r];
     real c0 = real(0.0), c1 = real(0.0);
     if (HAS_Y) {
       const real gr0 = sh.G2[row], gr1 = sh.G2[WS + row];
@@ -343,7 +349,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
         const real a = coef_a<NQ>(col, dt);
-        const real jb = sh.Jt[row * NX + coef_b<NQ>(col)];
+        const real jb = sh.Jt[row * JtStride<NX> + coef_b<NQ>(col)];
         real sacc = a != real(0.0) ? a * jb : real(0.0);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * WS + col];
