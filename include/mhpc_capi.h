@@ -192,7 +192,7 @@ void mhpc_destroy(mhpc_handle* h);
 #define MHPC_VARIANT_BWS 0            /* which: backward sweep */
 #define MHPC_VARIANT_BWS_1WAVE 1      /*   one wave per SIMD, no register cap */
 #define MHPC_VARIANT_BWS_2WAVE 2      /*   256-register build, two waves per SIMD */
-#define MHPC_VARIANT_BWS_PAIRWAVE 3   /*   two waves per problem (128-thread block) */
+#define MHPC_VARIANT_BWS_PAIRWAVE 3   /*   two waves per problem (128-thread block, one per SIMD) */
 #define MHPC_VARIANT_RO 1             /* which: line-search rollouts */
 #define MHPC_VARIANT_RO_PAIR 1        /*   two-wave pipeline, a lane pair per candidate */
 #define MHPC_VARIANT_RO_PIPE_STAGED 2 /*   two-wave pipeline, LDS-staged operands */

@@ -1070,9 +1070,13 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
   }
 }
 
-// Variant: sp.var_bws (mhpc_set_kernel_variant) or, by default, the 1-wave build while the
-// batch fits one wave per SIMD of the handle's device (sp.ncu), the 2-wave build beyond.
-// Both builds compile the same source; tests/test_gpu_variants.py checks them bit for bit.
+// Variant: sp.var_bws (mhpc_set_kernel_variant) or, by default by batch size on the
+// handle's device (sp.ncu CUs, 4 SIMDs each): two waves per problem (128-thread block, the
+// WB rounds' products split over twice the lanes: -20 % cycles per WB knot) while both fit
+// one SIMD each, the 1-wave build while one wave per problem does, the 2-wave (256-VGPR)
+// build beyond.  All builds compile the same source; tests/test_gpu_variants.py checks them
+// bit for bit.  The SRB half of a split sweep always runs 64-thread blocks (its rounds are
+// narrower than a wave).
 // part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).  The SRB half reads no
 // partials record and needs few registers (the WB code is not instantiated), so a partials
 // wave fits beside it on a SIMD.
@@ -1084,9 +1088,13 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
   (void)part;
 #else
   const int v = sp.var_bws ? sp.var_bws
-                           : sp.B <= 4 * sp.ncu ? MHPC_VARIANT_BWS_1WAVE : MHPC_VARIANT_BWS_2WAVE;
+                           : sp.B <= 2 * sp.ncu ? MHPC_VARIANT_BWS_PAIRWAVE
+                           : sp.B <= 4 * sp.ncu ? MHPC_VARIANT_BWS_1WAVE
+                                                : MHPC_VARIANT_BWS_2WAVE;
   if (part == 1)
     hipLaunchKernelGGL((k_bws<64, 2, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+  else if (v == MHPC_VARIANT_BWS_PAIRWAVE && part == 2)
+    hipLaunchKernelGGL((k_bws<128, 1, 2>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_1WAVE && part == 2)
     hipLaunchKernelGGL((k_bws<64, 1, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_2WAVE && part == 2)
@@ -1096,16 +1104,15 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
   else if (v == MHPC_VARIANT_BWS_2WAVE)
     hipLaunchKernelGGL((k_bws<64, 2, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else
-    hipLaunchKernelGGL((k_bws<128, 2, 0>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<128, 1, 0>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
 #endif
   return hipGetLastError();
 }
 
 // Whether the sweep runs as an SRB launch beside the partials and a WB launch after them:
-// both kinds of phase present, the 64-thread builds, not switched off (var_overlap 2).
+// both kinds of phase present, not switched off (var_overlap 2).
 bool bws_split(const SolveParams& sp) {
-  return sp.n_wb > 0 && sp.P > sp.n_wb && sp.var_overlap != 2 &&
-         sp.var_bws != MHPC_VARIANT_BWS_PAIRWAVE;
+  return sp.n_wb > 0 && sp.P > sp.n_wb && sp.var_overlap != 2;
 }
 
 }  // namespace MHPC_NS

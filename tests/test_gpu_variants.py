@@ -65,7 +65,8 @@ ALL_VARIANTS = [(b, r, "auto") for b, r in
                                   ("pair", "pipe_staged", "pipe", "fused_staged", "fused"))]
 # the backward sweep as one launch after the partials (the default splits it into an SRB
 # launch beside the partials and a WB launch after them)
-ALL_VARIANTS += [("1wave", "pair", "off"), ("2wave", "fused", "off"), ("auto", "auto", "off")]
+ALL_VARIANTS += [("1wave", "pair", "off"), ("2wave", "fused", "off"), ("pairwave", "pipe", "off"),
+                 ("auto", "auto", "off")]
 
 
 def test_variant_rejected_when_it_does_not_apply(need_gpu):
