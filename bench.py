@@ -168,6 +168,16 @@ def roofline_of(stats: dict, batch: int) -> dict:
          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
          "traffic_source": src, "alg_bytes_per_launch": bytes_per_launch,
          "avg_launch_ms": per_launch_s * 1e3}
+    # every kernel with an algorithmic byte model, for the kernels beside the dominant one
+    per = {}
+    for k, v in stats.items():
+        if v["launches"] <= 0 or v["alg_bytes"] <= 0 or v["ms"] <= 0:
+            continue
+        t = v["ms"] / 1e3 / v["launches"]
+        a = v["alg_bytes"] / v["launches"] / t / 1e9
+        per[k.split("(")[0]] = {"avg_launch_ms": t * 1e3, "achieved": a, "frac": a / HBM_PEAK_GBS,
+                                "traffic": load_pmc(k, batch)[0]}
+    r["per_kernel"] = per
     if flops_per_launch > 0 and per_launch_s > 0:
         tf = flops_per_launch / per_launch_s / 1e12
         r["valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",

@@ -171,8 +171,9 @@ int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, double* J, 
 /* Per-kernel device timing (HIP events around every launch on the handle's stream) and the
  * algorithmic HBM bytes each kernel must move (model in DESIGN.md §Roofline), accumulated
  * over all solves since the last reset.  Kernel ids: 0 init, 1 forward_sweep(0) cost,
- * 2 line search (rollouts + costs + selection), 3 partials, 4 backward_sweep, 5 al_update. */
-#define MHPC_NUM_KERNELS 6
+ * 2 line search (rollouts + costs + selection), 3 partials, 4 backward_sweep (whole, or its
+ * WB half when split), 5 al_update, 6 the SRB half of a split backward sweep. */
+#define MHPC_NUM_KERNELS 7
 const char* mhpc_kernel_name(int k);
 int mhpc_set_profiling(mhpc_handle* h, int on);
 int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches, double* alg_bytes);

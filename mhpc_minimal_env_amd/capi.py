@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MHPC_AMD_LIB") or os.path.join(HERE, "libmhpc_amd.so"
 MHPC_MAX_PHASES = 16
 MHPC_MAX_KNOTS = 1024
 MHPC_TRACE_LEN = 64
-MHPC_NUM_KERNELS = 6
+MHPC_NUM_KERNELS = 7
 MHPC_MAX_ROLLOUT_EPS = 4096
 
 MHPC_OK = 0

@@ -1053,6 +1053,7 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
     st->cnt[C_BWS_KNOTS_WB] += knots_wb;
     st->cnt[C_BWS_KNOTS_FB] += knots - knots_wb;
     st->cnt[C_PX_READS] += px_reads;
+    if (PART == 2) st->cnt[C_BWS_KNOTS_FB1] += d.carry[b].knots;
     st->bws_iter = bws_iter;
     if (aborted) {  // "Regularization term exceeds maximum value": return from solve()
       st->status = MHPC_SOLVE_REG_ABORT;

@@ -65,9 +65,9 @@ int fail(int code, const std::string& msg) {
   } while (0)
 }  // namespace
 
-enum { K_INIT = 0, K_FULL, K_LS, K_PAR, K_BWS, K_AL, NKERN };
+enum { K_INIT = 0, K_FULL, K_LS, K_PAR, K_BWS, K_AL, K_BWS_SRB, NKERN };
 static const char* kKernelNames[NKERN] = {"k_init", "k_cost(forward_sweep0)", "k_rollout(linesearch)",
-                                          "k_partials", "k_bws", "k_al_end"};
+                                          "k_partials", "k_bws", "k_al_end", "k_bws_srb"};
 
 struct Handle {
   mhpc_problem_desc desc;
@@ -429,7 +429,7 @@ static int solve_async(Handle* h) {
       LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 0, h->stream));
       return MHPC_OK;
     }
-    LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 1, h->stream));
+    LAUNCH(h, K_BWS_SRB, launch_bws(sp, d, o.update_regularization, 1, h->stream));
     HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
     LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 2, h->stream));
     return MHPC_OK;
@@ -482,10 +482,13 @@ int api_solve(Handle* h, int32_t* status) {
   h->kbytes[K_FULL] += c[C_FWD] * h->by_cost;
   h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read + c[C_LS_RUN] * h->by_roll_write;
   h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
-  h->kbytes[K_BWS] += c[C_BWS_KNOTS_WB] * kBwsWbKnot + c[C_BWS_KNOTS_FB] * kBwsFbKnot +
-                      c[C_PX_READS] * kBwsPx;
-  h->kflops[K_BWS] += c[C_BWS_KNOTS_WB] * kFlopWbKnot + c[C_BWS_KNOTS_FB] * kFlopFbKnot +
-                      c[C_PX_READS] * kFlopPx;
+  // the SRB half of a split sweep: the SRB knots of every first attempt; the rest (WB knots,
+  // impact steps, SRB knots of retries) is the WB half's / the whole sweep's
+  const unsigned long long fb1 = c[C_BWS_KNOTS_FB1], fb = c[C_BWS_KNOTS_FB] - fb1;
+  h->kbytes[K_BWS_SRB] += fb1 * kBwsFbKnot;
+  h->kflops[K_BWS_SRB] += fb1 * kFlopFbKnot;
+  h->kbytes[K_BWS] += c[C_BWS_KNOTS_WB] * kBwsWbKnot + fb * kBwsFbKnot + c[C_PX_READS] * kBwsPx;
+  h->kflops[K_BWS] += c[C_BWS_KNOTS_WB] * kFlopWbKnot + fb * kFlopFbKnot + c[C_PX_READS] * kFlopPx;
   if (status) {
     std::vector<ProbState> st(h->sp.B);
     D2H(st.data(), h->d.st, st.size() * sizeof(ProbState));

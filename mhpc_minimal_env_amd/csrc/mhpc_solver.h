@@ -40,7 +40,9 @@ constexpr int TRACE = MHPC_TRACE_LEN;
 // knot / Px counters feed the algorithmic-byte model of the roofline report.
 enum {
   C_DDP = 0, C_BWS, C_BWS_KNOTS, C_LS, C_FWD, C_PAR, C_LS_RUN, C_PAR_RUN,
-  C_LS_LAUNCH, C_BWS_KNOTS_WB, C_BWS_KNOTS_FB, C_PX_READS, NCNT
+  C_LS_LAUNCH, C_BWS_KNOTS_WB, C_BWS_KNOTS_FB, C_PX_READS,
+  C_BWS_KNOTS_FB1,  // SRB knots swept by the SRB half of a split sweep (its first attempt)
+  NCNT
 };
 
 struct SolveParams {

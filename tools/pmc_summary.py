@@ -24,6 +24,8 @@ def load(path, counter):
             name = r["Kernel_Name"]
             m = re.search(r"mhpc::(\w+)", name)
             key = m.group(1) if m else name
+            if key == "k_bws" and re.search(r"k_bws<\d+, \d+, 1>", name):
+                key = "k_bws_srb"  # SRB half of the split backward sweep
             acc[key].append(float(r["Counter_Value"]))
     return acc
 
