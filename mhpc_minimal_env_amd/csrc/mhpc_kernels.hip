@@ -101,7 +101,9 @@ __device__ __forceinline__ StageLane stage_lane(int lane) {
 // load is unconditional (lanes without an item re-read the chunk base, absent problems
 // problem 0's): a masked load would merge with the register's old value and make the
 // compiler wait for it on the spot, which is exactly the round trip the stage hides.
-template <bool WB>
+// NP: problem slots of the wave (ST_PPW; 3 in the pair variant, whose dynamics wave holds
+// 3 problems x 10 candidates) -- slots past NP would only load problem 0's data again.
+template <bool WB, int NP>
 __device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs& d,
                                             const StageLane& L, int b0, int ko, int k0, int nr,
                                             const int (&nomv)[ST_PPW], sreal2 (&pf)[ST_PPW * 3]) {
@@ -110,7 +112,7 @@ __device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs
   const int oB = L.kcB >= 0 && L.kcB < lim ? L.offB : 0;
   const int oC = L.kcC >= 0 && L.kcC < lim ? L.offC : 0;
 #pragma unroll
-  for (int lp = 0; lp < ST_PPW; ++lp) {
+  for (int lp = 0; lp < NP; ++lp) {
     const int nom = nomv[lp];  // < 0: problem absent or not iterating (uniform)
     const int bb = nom >= 0 ? b0 + lp : 0;
     const size_t kk = (size_t)bb * sp.NK + ko + k0;
@@ -124,10 +126,11 @@ __device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs
 }
 
 // Drop a loaded chunk into the LDS stage (lane-linear per slot).
+template <int NP>
 __device__ __forceinline__ void stage_drop(int lane, const sreal2 (&pf)[ST_PPW * 3],
                                            sreal2* stage2) {
 #pragma unroll
-  for (int i = 0; i < ST_PPW * 3; ++i) stage2[(i / 3) * ST_PAIRS + (i % 3) * 64 + lane] = pf[i];
+  for (int i = 0; i < NP * 3; ++i) stage2[(i / 3) * ST_PAIRS + (i % 3) * 64 + lane] = pf[i];
 }
 
 // Optional cycle accounting of the rollout's knot loop (build with -DMHPC_RO_TIMING, read
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   MHPC_NO_FMA_F32
   const int nc = full ? 1 : sp.n_cand;
   const int ppw = (PAIR ? 32 : 64) / nc;
+  constexpr int SNP = PAIR ? 3 : ST_PPW;  // staged problem slots (ppw <= SNP when staged)
   const int t = threadIdx.x, lane = t & 63;
   const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
   const int cl = (PAIR && w0) ? (lane >> 1) : lane;
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const bool sref = ST && N <= ST_RMAX;
     if (sref && w1) {
 #pragma unroll
-      for (int i = 0; i < ST_PPW * ST_RMAX / 64; ++i) {
+      for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
         const int f = lane + 64 * i, rl = f / ST_RMAX, rk = f - rl * ST_RMAX;
         if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
       }
@@ -252,8 +256,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
     sreal2 pf[ST_PPW * 3];
     if (ST && w0) {
-      if (wb) stage_issue<true>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
-      else stage_issue<false>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
+      if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
+      else stage_issue<false, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
     }
     for (int k = 0; k < N - 1; ++k, ++q) {
       const int s = PIPE ? (q & 1) : 0;
@@ -261,13 +265,13 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       const int kc = k & (CH - 1);
       RO_T(tk0);
       if (ST && w0 && kc == 0) {  // chunk boundary: drop the loaded chunk, fetch the next
-        stage_drop(lane, pf, stage2);
+        stage_drop<SNP>(lane, pf, stage2);
 #ifdef MHPC_RO_TIMING
         if (lane == 0) { const unsigned long long tdr = clock64(); ro_cyc[10] += tdr - tk0; }
 #endif
         if (k + CH < N - 1) {
-          if (wb) stage_issue<true>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
-          else stage_issue<false>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
+          if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
+          else stage_issue<false, SNP>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
         }
       }
 #ifdef MHPC_RO_TIMING
