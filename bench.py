@@ -207,12 +207,13 @@ def workload_text(name: str) -> str:
 class Solver:
     """One handle on this rank's GPU, stepping init + solve of its batch."""
 
-    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto")):
+    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0)):
         from mhpc_minimal_env_amd import capi
         from mhpc_minimal_env_amd import locomotion as L
         self.capi = capi
         self.loco = L.MHPCLocomotion(desc=desc, option=opt, batch=x0.shape[0], device=device)
-        self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2])
+        self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2],
+                                     sub_batches=variants[3])
         self.loco.set_initial_condition(x0)
         self.lib, self.h = capi.lib(), self.loco._h
         capi.check(self.lib.mhpc_set_x0(self.h, capi.dptr(self.loco._x0)), "mhpc_set_x0")
@@ -315,7 +316,8 @@ def run_sweep(args, torch):
     from mhpc_minimal_env_amd import configs
     desc, opt = workload(args.workload)
     for B in [int(b) for b in args.batch_sweep.split(",")]:
-        s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant, args.overlap))
+        s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant, args.overlap,
+                                                           args.sub_batches))
         for _ in range(args.warmup):
             s.step()
         s.loco.set_profiling(True)
@@ -375,6 +377,8 @@ def main():
                     help="pin the line-search launch variant (capi.RO_VARIANTS; tuning only)")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="partials beside the SRB half of the backward sweep (tuning only)")
+    ap.add_argument("--sub-batches", type=int, default=0,
+                    help="concurrently scheduled sub-batches per GPU, 1..4 (0 = automatic; tuning only)")
     ap.add_argument("--batch-sweep", default=None,
                     help="comma-separated batch sizes: one JSON line each (1 GPU)")
     args = ap.parse_args()
@@ -415,7 +419,8 @@ def main():
     x0 = configs.x0_for(desc, B, offset=rank * B)
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
-    s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant, args.overlap))
+    s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant, args.overlap,
+                                                           args.sub_batches))
     for _ in range(args.warmup):
         s.step()
     s.loco.set_profiling(True)

@@ -204,6 +204,12 @@ void mhpc_destroy(mhpc_handle* h);
 #define MHPC_VARIANT_OVERLAP_ON 1     /*   two launches + second stream (default when both
                                          WB and SRB phases are present) */
 #define MHPC_VARIANT_OVERLAP_OFF 2    /*   one sweep launch after the partials */
+#define MHPC_VARIANT_SUBBATCH 3       /* which: sub-batches run concurrently; variant = their
+                                         count 1..MHPC_MAX_SUBBATCH (contiguous blocks of the
+                                         batch, one stream pair each, staggered by one launch
+                                         so that one block's line search shares the chip with
+                                         another block's sweep); 0 = automatic */
+#define MHPC_MAX_SUBBATCH 4
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

@@ -29,6 +29,8 @@ BWS_VARIANTS = {"auto": 0, "1wave": 1, "2wave": 2, "pairwave": 3}
 RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged": 4, "fused": 5}
 MHPC_VARIANT_OVERLAP = 2
 OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}
+MHPC_VARIANT_SUBBATCH = 3
+MHPC_MAX_SUBBATCH = 4
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1
 MHPC_SOLVE_NONFINITE = 2

@@ -3,6 +3,7 @@
 // over a device-resident per-problem state machine).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -102,6 +103,15 @@ struct Handle {
   int nbk = 0, nk_cap = 0;
   bool need_full = false;
   bool store_valid = false;  // store zeroed since the last initialize (memory_reset)
+  // sub-batches (MHPC_VARIANT_SUBBATCH): the solve schedule runs once per contiguous block of
+  // problems, each block on its own stream pair; created on first use
+  int nsub_req = 0;
+  struct SubStreams {
+    hipStream_t s1 = nullptr, s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, gate = nullptr, done = nullptr;
+  };
+  std::vector<SubStreams> subs;
+  hipEvent_t evstart = nullptr;
 };
 
 // Phase layout of a descriptor: modes, knot counts and offsets, partials work items.
@@ -408,54 +418,176 @@ int api_initialize(Handle* h) {
 // skips the problems whose device state machine has left the corresponding loop.
 // With bws_split the partials of an iteration run on the second stream beside the SRB half
 // of the backward sweep (which reads no partials record); the WB half waits for them.
-static int solve_async(Handle* h) {
-  const SolveParams& sp = h->sp;
-  const DevBufs& d = h->d;
+//
+// Sub-batches (MHPC_VARIANT_SUBBATCH): the same schedule runs once per contiguous block of
+// problems, each block on its own stream pair.  Problems are independent and every array is
+// problem-major, so a block is a pointer offset and its problems compute exactly what they
+// compute in one launch over the whole batch (every launch shape is bitwise the same
+// arithmetic, tests/test_gpu_variants.py).  Block s+1 starts one launch behind block s:
+// the line search (two thirds of the SIMDs busy at batch 1024, one wave per SIMD) then
+// shares the chip with the other block's sweep / partials instead of leaving SIMDs idle.
+enum { OP_COST, OP_FULL, OP_PAR, OP_BWS, OP_LS, OP_AL };
+struct SolveOp {
+  int kind, al, ddp, max_ddp;
+};
+struct SolveBlock {
+  SolveParams sp;
+  DevBufs d;
+  hipStream_t s1, s2;
+  hipEvent_t fork, join;
+};
+
+// Problems [b0, b0 + sp.B) of the handle's arrays as the kernels index them (b * per-problem
+// stride, with sp.NK the knot stride of the packed arrays).
+static DevBufs block_bufs(const DevBufs& d, const SolveParams& sp, size_t b0) {
+  DevBufs o = d;
+  const size_t NK = sp.NK;
+  o.traj += b0 * sp.nslot * NK * KS;
+  o.refpos += b0 * NK;
+  o.K += b0 * NK * 56;
+  o.du += b0 * NK * 4;
+  o.G += b0 * NK * 14;
+  o.par += b0 * NK * PS;
+  o.px += b0 * MAXP * 196;
+  o.x0 += b0 * 14;
+  o.st += b0;
+  o.out += b0 * NK * KS;
+  o.carry += b0;
+  return o;
+}
+
+static std::vector<SolveOp> solve_ops(const Handle* h) {
   const mhpc_hsddp_option& o = h->opt;
-  const bool split = bws_split(sp);
-  auto partials = [&]() -> int {
-    if (!split) {
-      LAUNCH(h, K_PAR, launch_partials(sp, d, h->stream));
-      return MHPC_OK;
-    }
-    HIPCHK(hipEventRecord(h->evfork, h->stream));
-    HIPCHK(hipStreamWaitEvent(h->stream2, h->evfork, 0));
-    LAUNCH_ON(h, K_PAR, h->stream2, launch_partials(sp, d, h->stream2));
-    HIPCHK(hipEventRecord(h->evjoin, h->stream2));
-    return MHPC_OK;
-  };
-  auto bws = [&]() -> int {
-    if (!split) {
-      LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 0, h->stream));
-      return MHPC_OK;
-    }
-    LAUNCH(h, K_BWS_SRB, launch_bws(sp, d, o.update_regularization, 1, h->stream));
-    HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
-    LAUNCH(h, K_BWS, launch_bws(sp, d, o.update_regularization, 2, h->stream));
-    return MHPC_OK;
-  };
-  int rc;
+  std::vector<SolveOp> ops;
   int n_al = 0;
   for (int al = 1; al <= o.max_AL_iter; ++al) n_al = al;
-  for (int al = 1; al <= o.max_AL_iter; ++al) {
-    if (al == 1 && h->need_full)  // rotated nominal from update_problem: a real rollout
-      LAUNCH(h, K_FULL, launch_rollout(sp, d, al, 0, 0, 1, h->stream));
-    else
-      LAUNCH(h, K_FULL, launch_cost(sp, d, al, h->stream));  // forward_sweep(0)
-    if ((rc = partials())) return rc;
-    int max_ddp = 0;
-    for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
+  int max_ddp = 0;
+  for (int ddp = 1; ddp <= o.max_DDP_iter; ++ddp) max_ddp = ddp;
+  for (int al = 1; al <= n_al; ++al) {
+    // forward_sweep(0); a real rollout for the rotated nominal of update_problem
+    ops.push_back({al == 1 && h->need_full ? OP_FULL : OP_COST, al, 0, 0});
+    ops.push_back({OP_PAR, al, 0, 0});
     for (int ddp = 1; ddp <= max_ddp; ++ddp) {
-      if ((rc = bws())) return rc;
-      LAUNCH(h, K_LS, launch_rollout(sp, d, al, ddp, max_ddp, 0, h->stream));  // forward_iteration
-      if (ddp < max_ddp && (rc = partials())) return rc;
+      ops.push_back({OP_BWS, al, ddp, max_ddp});
+      ops.push_back({OP_LS, al, ddp, max_ddp});  // forward_iteration
+      if (ddp < max_ddp) ops.push_back({OP_PAR, al, ddp, max_ddp});
     }
-    LAUNCH(h, K_AL, launch_al_end(sp, d, al == n_al ? 1 : 0, h->stream));
+    ops.push_back({OP_AL, al == n_al ? 1 : 0, 0, 0});
   }
-  if (n_al == 0) LAUNCH(h, K_AL, launch_al_end(sp, d, 1, h->stream));
+  if (n_al == 0) ops.push_back({OP_AL, 1, 0, 0});
+  return ops;
+}
+
+// With bws_split the partials run on the block's second stream beside the SRB half of the
+// backward sweep (which reads no partials record); the WB half waits for them.
+static int issue_op(Handle* h, const SolveBlock& k, const SolveOp& op) {
+  const SolveParams& sp = k.sp;
+  const DevBufs& d = k.d;
+  const real ureg = h->opt.update_regularization;
+  const bool split = bws_split(sp);
+  switch (op.kind) {
+    case OP_FULL:
+      LAUNCH_ON(h, K_FULL, k.s1, launch_rollout(sp, d, op.al, 0, 0, 1, k.s1));
+      break;
+    case OP_COST:
+      LAUNCH_ON(h, K_FULL, k.s1, launch_cost(sp, d, op.al, k.s1));
+      break;
+    case OP_PAR:
+      if (!split) {
+        LAUNCH_ON(h, K_PAR, k.s1, launch_partials(sp, d, k.s1));
+        break;
+      }
+      HIPCHK(hipEventRecord(k.fork, k.s1));
+      HIPCHK(hipStreamWaitEvent(k.s2, k.fork, 0));
+      LAUNCH_ON(h, K_PAR, k.s2, launch_partials(sp, d, k.s2));
+      HIPCHK(hipEventRecord(k.join, k.s2));
+      break;
+    case OP_BWS:
+      if (!split) {
+        LAUNCH_ON(h, K_BWS, k.s1, launch_bws(sp, d, ureg, 0, k.s1));
+        break;
+      }
+      LAUNCH_ON(h, K_BWS_SRB, k.s1, launch_bws(sp, d, ureg, 1, k.s1));
+      HIPCHK(hipStreamWaitEvent(k.s1, k.join, 0));
+      LAUNCH_ON(h, K_BWS, k.s1, launch_bws(sp, d, ureg, 2, k.s1));
+      break;
+    case OP_LS:
+      LAUNCH_ON(h, K_LS, k.s1, launch_rollout(sp, d, op.al, op.ddp, op.max_ddp, 0, k.s1));
+      break;
+    default:
+      LAUNCH_ON(h, K_AL, k.s1, launch_al_end(sp, d, op.al, k.s1));
+  }
+  return MHPC_OK;
+}
+
+static int sub_batches(const Handle* h) {
+  int n = h->nsub_req;
+  if (n == 0) n = 1;  // automatic: one block (DESIGN.md §3 has the measured A/B)
+  return std::min(n, h->sp.B);
+}
+
+static int ensure_sub_streams(Handle* h, int n) {
+  if (!h->evstart) HIPCHK(hipEventCreateWithFlags(&h->evstart, hipEventDisableTiming));
+  while ((int)h->subs.size() < n) {
+    h->subs.emplace_back();
+    Handle::SubStreams& s = h->subs.back();
+    HIPCHK(hipStreamCreateWithFlags(&s.s1, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.s2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.gate, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  }
+  return MHPC_OK;
+}
+
+static int solve_async(Handle* h) {
+  const std::vector<SolveOp> ops = solve_ops(h);
+  const int nops = (int)ops.size();
+  const int nsub = sub_batches(h);
+  int rc;
+  if (nsub <= 1) {
+    const SolveBlock k{h->sp, h->d, h->stream, h->stream2, h->evfork, h->evjoin};
+    for (const SolveOp& op : ops)
+      if ((rc = issue_op(h, k, op))) return rc;
+  } else {
+    if ((rc = ensure_sub_streams(h, nsub))) return rc;
+    HIPCHK(hipEventRecord(h->evstart, h->stream));
+    std::vector<SolveBlock> blk(nsub);
+    const int bs = (h->sp.B + nsub - 1) / nsub;
+    for (int s = 0; s < nsub; ++s) {
+      const Handle::SubStreams& ss = h->subs[s];
+      SolveBlock& k = blk[s];
+      k.sp = h->sp;
+      k.sp.B = std::min(bs, h->sp.B - s * bs);
+      k.d = block_bufs(h->d, h->sp, (size_t)s * bs);
+      k.s1 = ss.s1;
+      k.s2 = ss.s2;
+      k.fork = ss.fork;
+      k.join = ss.join;
+      HIPCHK(hipStreamWaitEvent(k.s1, h->evstart, 0));
+    }
+    // block s runs `lag` launches behind block s - 1 (its first launch waits on the gate
+    // event recorded after launch lag - 1 of the block before; issued in that order)
+    int lag = 1;
+    if (const char* e = getenv("MHPC_SUB_LAG")) lag = atoi(e);  // tuning only
+    lag = std::max(0, std::min(lag, nops - 1));
+    for (int t = 0; t < nops + (nsub - 1) * lag; ++t)
+      for (int s = 0; s < nsub; ++s) {
+        const int i = t - s * lag;
+        if (i < 0 || i >= nops) continue;
+        if (s > 0 && i == 0 && lag > 0) HIPCHK(hipStreamWaitEvent(blk[s].s1, h->subs[s - 1].gate, 0));
+        if ((rc = issue_op(h, blk[s], ops[i]))) return rc;
+        if (s + 1 < nsub && lag > 0 && i == lag - 1) HIPCHK(hipEventRecord(h->subs[s].gate, blk[s].s1));
+      }
+    for (int s = 0; s < nsub; ++s) {
+      HIPCHK(hipEventRecord(h->subs[s].done, blk[s].s1));
+      HIPCHK(hipStreamWaitEvent(h->stream, h->subs[s].done, 0));
+    }
+  }
   // batch totals of the per-problem counters (tiny reduction, NCNT words back)
   HIPCHK(hipMemsetAsync(h->dcnt, 0, NCNT * sizeof(unsigned long long), h->stream));
-  HIPCHK(launch_reduce_counters(sp, d, h->dcnt, h->stream));
+  HIPCHK(launch_reduce_counters(h->sp, h->d, h->dcnt, h->stream));
   return MHPC_OK;
 }
 
@@ -759,6 +891,11 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
     sp.var_overlap = variant;
     return MHPC_OK;
   }
+  if (which == MHPC_VARIANT_SUBBATCH) {
+    if (variant < 0 || variant > MHPC_MAX_SUBBATCH) return fail(MHPC_ERR_INVALID, "sub-batch count must be 0..4");
+    h->nsub_req = variant;
+    return MHPC_OK;
+  }
   if (which != MHPC_VARIANT_RO) return fail(MHPC_ERR_INVALID, "no such kernel");
   if (variant < 0 || variant > MHPC_VARIANT_RO_FUSED) return fail(MHPC_ERR_INVALID, "no such line-search variant");
   const bool staged = variant == MHPC_VARIANT_RO_PAIR || variant == MHPC_VARIANT_RO_PIPE_STAGED ||
@@ -799,6 +936,16 @@ void api_destroy(Handle* h) {
   if (h->evjoin) (void)hipEventDestroy(h->evjoin);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  for (Handle::SubStreams& s : h->subs) {
+    for (hipStream_t q : {s.s1, s.s2})
+      if (q) {
+        (void)hipStreamSynchronize(q);
+        (void)hipStreamDestroy(q);
+      }
+    for (hipEvent_t e : {s.fork, s.join, s.gate, s.done})
+      if (e) (void)hipEventDestroy(e);
+  }
+  if (h->evstart) (void)hipEventDestroy(h->evstart);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
