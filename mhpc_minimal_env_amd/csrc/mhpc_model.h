@@ -134,9 +134,12 @@ MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, real l1, real l2, Q jx[5], Q jz
 // Packed lower-triangular index of the symmetric 7x7 mass matrix.
 MHPC_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
-// Contribution of the thigh and shank of leg F to M (packed) and h.  xv = qdot.
+// Contribution of the thigh and shank of leg F to M (packed) and h.  xv = qdot.  The
+// entries shared with the other leg -- M(2, 0..2) and h(0..2) -- are returned per leg as
+// thigh + shank (bm, bh) and summed by the caller as front + back: a sum of two terms is
+// the same whichever lane of the line search's lane pair holds which (mhpc_model_pair.h).
 template <class Q, class V, int F>
-MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
+MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7], Q bm[3], V bh[3]) {
   MHPC_NO_FMA_WB
   constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
   constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
@@ -162,7 +165,9 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
 #pragma unroll
     for (int a = 0; a < 5; ++a) {
       if (a >= nc) continue;
-      h[idx[a]] += m * (jx[a] * ax + jz[a] * az);
+      const V dh = m * (jx[a] * ax + jz[a] * az);
+      if (a < 3) bh[a] = b == 0 ? dh : bh[a] + dh;
+      else h[idx[a]] += dh;
 #pragma unroll
       for (int c = 0; c <= a; ++c) {
         // x/z columns of a CoM Jacobian are unit vectors: skip the exact zeros
@@ -172,7 +177,8 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
         }
         Q v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
         if (a >= 2 && c >= 2) v += ic;
-        M[tri(idx[a], idx[c])] += v;
+        if (a == 2) bm[c] = b == 0 ? v : bm[c] + v;
+        else M[tri(idx[a], idx[c])] += v;
       }
     }
   }
@@ -187,10 +193,18 @@ MHPC_HD void wb_mass_bias(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7]) {
   for (int i = 0; i < 28; ++i) M[i] = Q(real(0.0));
   M[tri(0, 0)] = Q(kBodyMass);
   M[tri(1, 1)] = Q(kBodyMass);
-  M[tri(2, 2)] = Q(kBodyInertia);
-  h[1] = V(kBodyMass * kGrav);
-  add_leg<Q, V, kFront>(xv, g, M, h);
-  add_leg<Q, V, kBack>(xv, g, M, h);
+  Q bmf[3], bmb[3];
+  V bhf[3], bhb[3];
+  add_leg<Q, V, kFront>(xv, g, M, h, bmf, bhf);
+  add_leg<Q, V, kBack>(xv, g, M, h, bmb, bhb);
+  // shared entries: constant + (front + back)
+  const real m2[3] = {real(0.0), real(0.0), kBodyInertia};
+  const real h0[3] = {real(0.0), kBodyMass * kGrav, real(0.0)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    M[tri(2, c)] = Q(m2[c]) + (bmf[c] + bmb[c]);
+    h[c] = V(h0[c]) + (bhf[c] + bhb[c]);
+  }
 }
 
 // Block-arrowhead factorisation of the mass matrix.  Ordered (base x,z,th | front leg |
@@ -210,6 +224,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   // base Schur complement S = Mbb - sum_l Mlb' Ml^-1 Mlb (symmetric, lower packed)
   S s00 = M[tri(0, 0)], s10 = M[tri(1, 0)], s11 = M[tri(1, 1)];
   S s20 = M[tri(2, 0)], s21 = M[tri(2, 1)], s22 = M[tri(2, 2)];
+  S t[2][6];
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
@@ -224,16 +239,23 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
       F.Z[l][0][j] = F.Li[l][0] * m0 + F.Li[l][1] * m1;
       F.Z[l][1][j] = F.Li[l][1] * m0 + F.Li[l][2] * m1;
     }
-    // S -= Mlb' Z
+    // leg l's term of S -= sum_l Mlb' Z_l
     const S* z0 = F.Z[l][0];
     const S* z1 = F.Z[l][1];
-    s00 -= M[tri(i0, 0)] * z0[0] + M[tri(i1, 0)] * z1[0];
-    s10 -= M[tri(i0, 1)] * z0[0] + M[tri(i1, 1)] * z1[0];
-    s11 -= M[tri(i0, 1)] * z0[1] + M[tri(i1, 1)] * z1[1];
-    s20 -= M[tri(i0, 2)] * z0[0] + M[tri(i1, 2)] * z1[0];
-    s21 -= M[tri(i0, 2)] * z0[1] + M[tri(i1, 2)] * z1[1];
-    s22 -= M[tri(i0, 2)] * z0[2] + M[tri(i1, 2)] * z1[2];
+    t[l][0] = M[tri(i0, 0)] * z0[0] + M[tri(i1, 0)] * z1[0];
+    t[l][1] = M[tri(i0, 1)] * z0[0] + M[tri(i1, 1)] * z1[0];
+    t[l][2] = M[tri(i0, 1)] * z0[1] + M[tri(i1, 1)] * z1[1];
+    t[l][3] = M[tri(i0, 2)] * z0[0] + M[tri(i1, 2)] * z1[0];
+    t[l][4] = M[tri(i0, 2)] * z0[1] + M[tri(i1, 2)] * z1[1];
+    t[l][5] = M[tri(i0, 2)] * z0[2] + M[tri(i1, 2)] * z1[2];
   }
+  // front + back (see add_leg)
+  s00 -= t[0][0] + t[1][0];
+  s10 -= t[0][1] + t[1][1];
+  s11 -= t[0][2] + t[1][2];
+  s20 -= t[0][3] + t[1][3];
+  s21 -= t[0][4] + t[1][4];
+  s22 -= t[0][5] + t[1][5];
   // 3x3 symmetric inverse by cofactors
   const S c00 = s11 * s22 - s21 * s21;
   const S c10 = s21 * s20 - s10 * s22;
@@ -251,17 +273,20 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
 template <class Q, class V>
 MHPC_HD void arrow_solve(const Q M[28], const ArrowFactor<Q>& F, V b[7]) {
   MHPC_NO_FMA_WB
-  V w[2][2];
-  V r0 = b[0], r1 = b[1], r2 = b[2];
+  V w[2][2], t[2][3];
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
     w[l][0] = F.Li[l][0] * b[i0] + F.Li[l][1] * b[i1];
     w[l][1] = F.Li[l][1] * b[i0] + F.Li[l][2] * b[i1];
-    r0 -= M[tri(i0, 0)] * w[l][0] + M[tri(i1, 0)] * w[l][1];
-    r1 -= M[tri(i0, 1)] * w[l][0] + M[tri(i1, 1)] * w[l][1];
-    r2 -= M[tri(i0, 2)] * w[l][0] + M[tri(i1, 2)] * w[l][1];
+    t[l][0] = M[tri(i0, 0)] * w[l][0] + M[tri(i1, 0)] * w[l][1];
+    t[l][1] = M[tri(i0, 1)] * w[l][0] + M[tri(i1, 1)] * w[l][1];
+    t[l][2] = M[tri(i0, 2)] * w[l][0] + M[tri(i1, 2)] * w[l][1];
   }
+  // base rows minus front + back (see add_leg)
+  const V r0 = b[0] - (t[0][0] + t[1][0]);
+  const V r1 = b[1] - (t[0][1] + t[1][1]);
+  const V r2 = b[2] - (t[0][2] + t[1][2]);
   const V x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
   const V x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
   const V x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;

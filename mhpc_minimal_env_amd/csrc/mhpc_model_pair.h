@@ -23,9 +23,9 @@ namespace MHPC_NS {
 MHPC_HD double pair_swap(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, 0xB1, 0xF, 0xF, false);
-  const unsigned hi =
-      (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), 0xB1, 0xF, 0xF, false);
+  // mov_dpp: no "old" operand to materialise (every lane has a valid source in a quad_perm)
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, 0xB1, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), 0xB1, 0xF, 0xF, false);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 #elif defined(MHPC_PAIR_HOST_SWAP)
   return mhpc_host_pair_swap(v);  // test-only host emulation of the lane pair (two threads)
@@ -35,7 +35,7 @@ MHPC_HD double pair_swap(double v) {
 }
 MHPC_HD float pair_swap(float v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
 #elif defined(MHPC_PAIR_HOST_SWAP)
   return (float)mhpc_host_pair_swap((double)v);
 #else
@@ -131,6 +131,13 @@ MHPC_HD void pair_order(bool back, real own, real* fr, real* bk) {
   *bk = back ? own : oth;
 }
 
+// front + back of a per-leg quantity, the same on both lanes without ordering them: a sum
+// of two terms does not depend on their order (the single-lane model sums front + back).
+MHPC_HD real pair_sum(real own) {
+  MHPC_NO_FMA_WB
+  return own + pair_swap(own);
+}
+
 // Arrowhead solve of the pair: rhs = (base part rb[3] identical on both lanes, own-leg
 // part rl[2]); returns the base result xb[3] (identical on both lanes) and the own-leg
 // result xl[2].  Same operations and order as arrow_solve.
@@ -148,13 +155,8 @@ MHPC_HD void pair_solve(const PairFactor& F, bool back, const real rb[3],
   const real t0 = F.Mh[0] * w0 + F.Mk[0] * w1;
   const real t1 = F.Mh[1] * w0 + F.Mk[1] * w1;
   const real t2 = F.Mh[2] * w0 + F.Mk[2] * w1;
-  real f0, b0, f1, b1, f2, b2;
-  pair_order(back, t0, &f0, &b0);
-  pair_order(back, t1, &f1, &b1);
-  pair_order(back, t2, &f2, &b2);
-  real r0 = rb[0], r1 = rb[1], r2 = rb[2];
-  r0 -= f0; r1 -= f1; r2 -= f2;
-  r0 -= b0; r1 -= b1; r2 -= b2;
+  // base rows minus front + back (arrow_solve)
+  const real r0 = rb[0] - pair_sum(t0), r1 = rb[1] - pair_sum(t1), r2 = rb[2] - pair_sum(t2);
   const real x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
   const real x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
   const real x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
@@ -183,18 +185,13 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   L.w2 = L.w1 + qkd;
   PairLegMH lm;
   pair_leg_mass_bias(L, sg, sth, cth, x[9], lm);
-  // base block and base bias: body constants, then front thigh, front shank, back thigh,
-  // back shank (wb_mass_bias + add_leg order)
+  // base block and base bias: body constant + (front leg + back leg), each leg thigh +
+  // shank (wb_mass_bias + add_leg order)
   real bs[6];  // M20, M21, M22, h0, h1, h2
   const real init[6] = {real(0.0), real(0.0), kBodyInertia, real(0.0), kBodyMass * kGrav,
                         real(0.0)};
 #pragma unroll
-  for (int e = 0; e < 6; ++e) {
-    real fT, bT, fS, bS;
-    pair_order(back, lm.base[0][e], &fT, &bT);
-    pair_order(back, lm.base[1][e], &fS, &bS);
-    bs[e] = (((init[e] + fT) + fS) + bT) + bS;
-  }
+  for (int e = 0; e < 6; ++e) bs[e] = init[e] + pair_sum(lm.base[0][e] + lm.base[1][e]);
   // M00 = M11 = body + leg masses (constant), M10 = 0
   real M00 = kBodyMass, M11 = kBodyMass;
   M00 += kThighMass; M11 += kThighMass;
@@ -226,12 +223,7 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
                      lm.Mh[2] * z0[1] + lm.Mk[2] * z1[1], lm.Mh[2] * z0[2] + lm.Mk[2] * z1[2]};
   real s[6] = {M00, M10, M11, M20, M21, M22};  // s00, s10, s11, s20, s21, s22
 #pragma unroll
-  for (int e = 0; e < 6; ++e) {
-    real tf, tb;
-    pair_order(back, t[e], &tf, &tb);
-    s[e] -= tf;
-    s[e] -= tb;
-  }
+  for (int e = 0; e < 6; ++e) s[e] -= pair_sum(t[e]);  // minus front + back (arrow_factor)
   {
     const real s00 = s[0], s10 = s[1], s11 = s[2], s20 = s[3], s21 = s[4], s22 = s[5];
     const real c00 = s11 * s22 - s21 * s21;
