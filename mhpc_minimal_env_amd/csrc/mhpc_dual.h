@@ -64,6 +64,19 @@ MHPC_HD Dual& operator+=(Dual& a, Dual b) { a = a + b; return a; }
 MHPC_HD Dual& operator-=(Dual& a, Dual b) { a = a - b; return a; }
 MHPC_HD Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
 
+// Fused a * b + c, written out where the whole-body models want it: the models are compiled
+// without contraction (MHPC_NO_FMA_WB, so that the line search's lane pair and the single
+// lane round alike), and every fused product is spelled the same way in both.  Dual: the
+// primal fused, the tangent (a b)' + c' (the partials compare to the reference at 1e-9).
+MHPC_HD real mad(real a, real b, real c) { return fma(a, b, c); }
+MHPC_HD Dual mad(Dual a, Dual b, Dual c) { return Dual(fma(a.v, b.v, c.v), fma(a.d, b.v, fma(a.v, b.d, c.d))); }
+MHPC_HD Dual mad(real a, Dual b, Dual c) { return Dual(fma(a, b.v, c.v), fma(a, b.d, c.d)); }
+MHPC_HD Dual mad(Dual a, real b, Dual c) { return Dual(fma(a.v, b, c.v), fma(a.d, b, c.d)); }
+MHPC_HD Dual mad(Dual a, Dual b, real c) { return Dual(fma(a.v, b.v, c), fma(a.d, b.v, a.v * b.d)); }
+MHPC_HD Dual mad(real a, real b, Dual c) { return Dual(fma(a, b, c.v), c.d); }
+MHPC_HD Dual mad(real a, Dual b, real c) { return Dual(fma(a, b.v, c), a * b.d); }
+MHPC_HD Dual mad(Dual a, real b, real c) { return Dual(fma(a.v, b, c), a.d * b); }
+
 // Scalar-generic elementary functions (real and Dual share the model source).
 MHPC_HD real val(real a) { return a; }
 MHPC_HD real val(Dual a) { return a.v; }

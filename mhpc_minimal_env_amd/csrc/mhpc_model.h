@@ -125,10 +125,10 @@ MHPC_HD void leg_point_jac(const WbGeo<Q, V>& g, real l1, real l2, Q jx[5], Q jz
   jx[4] = tx2;    jz[4] = tz2;
   jx[3] = tx1 + tx2;
   jz[3] = tz1 + tz2;
-  jx[2] = (-sg * kHipX) * g.sth + jx[3];
-  jz[2] = (-sg * kHipX) * g.cth + jz[3];
-  *jdx = L.w1 * L.w1 * (l1 * L.s1) + L.w2 * L.w2 * (l2 * L.s2);
-  *jdz = L.w1 * L.w1 * (l1 * L.c1) + L.w2 * L.w2 * (l2 * L.c2);
+  jx[2] = mad(-sg * kHipX, g.sth, jx[3]);
+  jz[2] = mad(-sg * kHipX, g.cth, jz[3]);
+  *jdx = mad(L.w1 * L.w1, l1 * L.s1, L.w2 * L.w2 * (l2 * L.s2));
+  *jdz = mad(L.w1 * L.w1, l1 * L.c1, L.w2 * L.w2 * (l2 * L.c2));
 }
 
 // Packed lower-triangular index of the symmetric 7x7 mass matrix.
@@ -165,7 +165,7 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7], Q bm[3]
 #pragma unroll
     for (int a = 0; a < 5; ++a) {
       if (a >= nc) continue;
-      const V dh = m * (jx[a] * ax + jz[a] * az);
+      const V dh = m * mad(jx[a], ax, jz[a] * az);
       if (a < 3) bh[a] = b == 0 ? dh : bh[a] + dh;
       else h[idx[a]] += dh;
 #pragma unroll
@@ -175,7 +175,7 @@ MHPC_HD void add_leg(const V* xv, const WbGeo<Q, V>& g, Q M[28], V h[7], Q bm[3]
           if (a == c) M[tri(idx[a], idx[c])] += Q(m);
           continue;
         }
-        Q v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
+        Q v = m * mad(jx[a], jx[c], jz[a] * jz[c]);
         if (a >= 2 && c >= 2) v += ic;
         if (a == 2) bm[c] = b == 0 ? v : bm[c] + v;
         else M[tri(idx[a], idx[c])] += v;
@@ -229,25 +229,25 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
     const S a = M[tri(i0, i0)], b = M[tri(i1, i0)], c = M[tri(i1, i1)];
-    const S rdet = S(real(1.0)) / (a * c - b * b);
+    const S rdet = S(real(1.0)) / mad(a, c, -(b * b));
     F.Li[l][0] = c * rdet;
     F.Li[l][1] = -b * rdet;
     F.Li[l][2] = a * rdet;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const S m0 = M[tri(i0, j)], m1 = M[tri(i1, j)];
-      F.Z[l][0][j] = F.Li[l][0] * m0 + F.Li[l][1] * m1;
-      F.Z[l][1][j] = F.Li[l][1] * m0 + F.Li[l][2] * m1;
+      F.Z[l][0][j] = mad(F.Li[l][0], m0, F.Li[l][1] * m1);
+      F.Z[l][1][j] = mad(F.Li[l][1], m0, F.Li[l][2] * m1);
     }
     // leg l's term of S -= sum_l Mlb' Z_l
     const S* z0 = F.Z[l][0];
     const S* z1 = F.Z[l][1];
-    t[l][0] = M[tri(i0, 0)] * z0[0] + M[tri(i1, 0)] * z1[0];
-    t[l][1] = M[tri(i0, 1)] * z0[0] + M[tri(i1, 1)] * z1[0];
-    t[l][2] = M[tri(i0, 1)] * z0[1] + M[tri(i1, 1)] * z1[1];
-    t[l][3] = M[tri(i0, 2)] * z0[0] + M[tri(i1, 2)] * z1[0];
-    t[l][4] = M[tri(i0, 2)] * z0[1] + M[tri(i1, 2)] * z1[1];
-    t[l][5] = M[tri(i0, 2)] * z0[2] + M[tri(i1, 2)] * z1[2];
+    t[l][0] = mad(M[tri(i0, 0)], z0[0], M[tri(i1, 0)] * z1[0]);
+    t[l][1] = mad(M[tri(i0, 1)], z0[0], M[tri(i1, 1)] * z1[0]);
+    t[l][2] = mad(M[tri(i0, 1)], z0[1], M[tri(i1, 1)] * z1[1]);
+    t[l][3] = mad(M[tri(i0, 2)], z0[0], M[tri(i1, 2)] * z1[0]);
+    t[l][4] = mad(M[tri(i0, 2)], z0[1], M[tri(i1, 2)] * z1[1]);
+    t[l][5] = mad(M[tri(i0, 2)], z0[2], M[tri(i1, 2)] * z1[2]);
   }
   // front + back (see add_leg)
   s00 -= t[0][0] + t[1][0];
@@ -257,16 +257,16 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   s21 -= t[0][4] + t[1][4];
   s22 -= t[0][5] + t[1][5];
   // 3x3 symmetric inverse by cofactors
-  const S c00 = s11 * s22 - s21 * s21;
-  const S c10 = s21 * s20 - s10 * s22;
-  const S c20 = s10 * s21 - s11 * s20;
-  const S rdet = S(real(1.0)) / (s00 * c00 + s10 * c10 + s20 * c20);
+  const S c00 = mad(s11, s22, -(s21 * s21));
+  const S c10 = mad(s21, s20, -(s10 * s22));
+  const S c20 = mad(s10, s21, -(s11 * s20));
+  const S rdet = S(real(1.0)) / mad(s20, c20, mad(s10, c10, s00 * c00));
   F.Si[0] = c00 * rdet;
   F.Si[1] = c10 * rdet;
-  F.Si[2] = (s00 * s22 - s20 * s20) * rdet;
+  F.Si[2] = mad(s00, s22, -(s20 * s20)) * rdet;
   F.Si[3] = c20 * rdet;
-  F.Si[4] = (s20 * s10 - s00 * s21) * rdet;
-  F.Si[5] = (s00 * s11 - s10 * s10) * rdet;
+  F.Si[4] = mad(s20, s10, -(s00 * s21)) * rdet;
+  F.Si[5] = mad(s00, s11, -(s10 * s10)) * rdet;
 }
 
 // b <- M^-1 b  (M, factor in Q; b in V)
@@ -277,26 +277,26 @@ MHPC_HD void arrow_solve(const Q M[28], const ArrowFactor<Q>& F, V b[7]) {
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
-    w[l][0] = F.Li[l][0] * b[i0] + F.Li[l][1] * b[i1];
-    w[l][1] = F.Li[l][1] * b[i0] + F.Li[l][2] * b[i1];
-    t[l][0] = M[tri(i0, 0)] * w[l][0] + M[tri(i1, 0)] * w[l][1];
-    t[l][1] = M[tri(i0, 1)] * w[l][0] + M[tri(i1, 1)] * w[l][1];
-    t[l][2] = M[tri(i0, 2)] * w[l][0] + M[tri(i1, 2)] * w[l][1];
+    w[l][0] = mad(F.Li[l][0], b[i0], F.Li[l][1] * b[i1]);
+    w[l][1] = mad(F.Li[l][1], b[i0], F.Li[l][2] * b[i1]);
+    t[l][0] = mad(M[tri(i0, 0)], w[l][0], M[tri(i1, 0)] * w[l][1]);
+    t[l][1] = mad(M[tri(i0, 1)], w[l][0], M[tri(i1, 1)] * w[l][1]);
+    t[l][2] = mad(M[tri(i0, 2)], w[l][0], M[tri(i1, 2)] * w[l][1]);
   }
   // base rows minus front + back (see add_leg)
   const V r0 = b[0] - (t[0][0] + t[1][0]);
   const V r1 = b[1] - (t[0][1] + t[1][1]);
   const V r2 = b[2] - (t[0][2] + t[1][2]);
-  const V x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
-  const V x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
-  const V x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
+  const V x0 = mad(F.Si[3], r2, mad(F.Si[1], r1, F.Si[0] * r0));
+  const V x1 = mad(F.Si[4], r2, mad(F.Si[2], r1, F.Si[1] * r0));
+  const V x2 = mad(F.Si[5], r2, mad(F.Si[4], r1, F.Si[3] * r0));
   b[0] = x0;
   b[1] = x1;
   b[2] = x2;
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
-    b[3 + 2 * l] = w[l][0] - (F.Z[l][0][0] * x0 + F.Z[l][0][1] * x1 + F.Z[l][0][2] * x2);
-    b[4 + 2 * l] = w[l][1] - (F.Z[l][1][0] * x0 + F.Z[l][1][1] * x1 + F.Z[l][1][2] * x2);
+    b[3 + 2 * l] = w[l][0] - mad(F.Z[l][0][2], x2, mad(F.Z[l][0][1], x1, F.Z[l][0][0] * x0));
+    b[4 + 2 * l] = w[l][1] - mad(F.Z[l][1][2], x2, mad(F.Z[l][1][1], x1, F.Z[l][1][0] * x0));
   }
 }
 
@@ -336,17 +336,17 @@ MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7]
   V r0 = -c[0], r1 = -c[1];
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
-    A00 += J[0][i] * Y[0][i];
-    A01 += J[0][i] * Y[1][i];
-    A11 += J[1][i] * Y[1][i];
-    r0 -= J[0][i] * v[i];
-    r1 -= J[1][i] * v[i];
+    A00 = mad(J[0][i], Y[0][i], A00);
+    A01 = mad(J[0][i], Y[1][i], A01);
+    A11 = mad(J[1][i], Y[1][i], A11);
+    r0 = mad(-J[0][i], v[i], r0);
+    r1 = mad(-J[1][i], v[i], r1);
   }
-  const Q rdet = Q(real(1.0)) / (A00 * A11 - A01 * A01);
-  lam[0] = (A11 * r0 - A01 * r1) * rdet;
-  lam[1] = (A00 * r1 - A01 * r0) * rdet;
+  const Q rdet = Q(real(1.0)) / mad(A00, A11, -(A01 * A01));
+  lam[0] = mad(A11, r0, -(A01 * r1)) * rdet;
+  lam[1] = mad(A00, r1, -(A01 * r0)) * rdet;
 #pragma unroll
-  for (int i = 0; i < 7; ++i) v[i] += Y[0][i] * lam[0] + Y[1][i] * lam[1];
+  for (int i = 0; i < 7; ++i) v[i] += mad(Y[0][i], lam[0], Y[1][i] * lam[1]);
 }
 
 // Stance dynamics with foot F on the ground (Dyn_FS: F = front, Dyn_BS: F = back).

@@ -56,10 +56,10 @@ MHPC_HD void pair_point_jac(const LegGeo<real, real>& L, real sg, real sth,
   jx[4] = tx2;    jz[4] = tz2;
   jx[3] = tx1 + tx2;
   jz[3] = tz1 + tz2;
-  jx[2] = (-sg * kHipX) * sth + jx[3];
-  jz[2] = (-sg * kHipX) * cth + jz[3];
-  *jdx = L.w1 * L.w1 * (l1 * L.s1) + L.w2 * L.w2 * (l2 * L.s2);
-  *jdz = L.w1 * L.w1 * (l1 * L.c1) + L.w2 * L.w2 * (l2 * L.c2);
+  jx[2] = mad(-sg * kHipX, sth, jx[3]);
+  jz[2] = mad(-sg * kHipX, cth, jz[3]);
+  *jdx = mad(L.w1 * L.w1, l1 * L.s1, L.w2 * L.w2 * (l2 * L.s2));
+  *jdz = mad(L.w1 * L.w1, l1 * L.c1, L.w2 * L.w2 * (l2 * L.c2));
 }
 
 // Own-leg part of M and h (add_leg): the base entries per body (M(2,0), M(2,1), M(2,2),
@@ -102,13 +102,13 @@ MHPC_HD void pair_leg_mass_bias(const LegGeo<real, real>& L, real sg, real sth,
 #pragma unroll
     for (int a = 0; a < 5; ++a) {
       if (a >= nc) continue;
-      const real dh = m * (jx[a] * ax + jz[a] * az);
+      const real dh = m * mad(jx[a], ax, jz[a] * az);
       if (a < 3) bb[3 + a] = dh;
       else hl[a] += dh;
 #pragma unroll
       for (int c = 0; c <= a; ++c) {
         if (a < 2 && c < 2) continue;  // constant entries (the body masses), summed by the caller
-        real v = m * (jx[a] * jx[c] + jz[a] * jz[c]);
+        real v = m * mad(jx[a], jx[c], jz[a] * jz[c]);
         if (a >= 2 && c >= 2) v += ic;
         if (a == 2) bb[c] = v;  // M(2, c), c = 0, 1, 2
         else Ml[a][c] += v;
@@ -150,19 +150,19 @@ struct PairFactor {
 MHPC_HD void pair_solve(const PairFactor& F, bool back, const real rb[3],
                                            const real rl[2], real xb[3], real xl[2]) {
   MHPC_NO_FMA_WB
-  const real w0 = F.Li[0] * rl[0] + F.Li[1] * rl[1];
-  const real w1 = F.Li[1] * rl[0] + F.Li[2] * rl[1];
-  const real t0 = F.Mh[0] * w0 + F.Mk[0] * w1;
-  const real t1 = F.Mh[1] * w0 + F.Mk[1] * w1;
-  const real t2 = F.Mh[2] * w0 + F.Mk[2] * w1;
+  const real w0 = mad(F.Li[0], rl[0], F.Li[1] * rl[1]);
+  const real w1 = mad(F.Li[1], rl[0], F.Li[2] * rl[1]);
+  const real t0 = mad(F.Mh[0], w0, F.Mk[0] * w1);
+  const real t1 = mad(F.Mh[1], w0, F.Mk[1] * w1);
+  const real t2 = mad(F.Mh[2], w0, F.Mk[2] * w1);
   // base rows minus front + back (arrow_solve)
   const real r0 = rb[0] - pair_sum(t0), r1 = rb[1] - pair_sum(t1), r2 = rb[2] - pair_sum(t2);
-  const real x0 = F.Si[0] * r0 + F.Si[1] * r1 + F.Si[3] * r2;
-  const real x1 = F.Si[1] * r0 + F.Si[2] * r1 + F.Si[4] * r2;
-  const real x2 = F.Si[3] * r0 + F.Si[4] * r1 + F.Si[5] * r2;
+  const real x0 = mad(F.Si[3], r2, mad(F.Si[1], r1, F.Si[0] * r0));
+  const real x1 = mad(F.Si[4], r2, mad(F.Si[2], r1, F.Si[1] * r0));
+  const real x2 = mad(F.Si[5], r2, mad(F.Si[4], r1, F.Si[3] * r0));
   xb[0] = x0; xb[1] = x1; xb[2] = x2;
-  xl[0] = w0 - (F.Z[0][0] * x0 + F.Z[0][1] * x1 + F.Z[0][2] * x2);
-  xl[1] = w1 - (F.Z[1][0] * x0 + F.Z[1][1] * x1 + F.Z[1][2] * x2);
+  xl[0] = w0 - mad(F.Z[0][2], x2, mad(F.Z[0][1], x1, F.Z[0][0] * x0));
+  xl[1] = w1 - mad(F.Z[1][2], x2, mad(F.Z[1][1], x1, F.Z[1][0] * x0));
 }
 
 // x (14, identical on both lanes of the pair), u_own = the own leg's two joint torques.
@@ -203,39 +203,39 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   PairFactor F;
   {
     const real a = lm.Mhh, b = lm.Mkh, c = lm.Mkk;
-    const real rdet = real(1.0) / (a * c - b * b);
+    const real rdet = real(1.0) / mad(a, c, -(b * b));
     F.Li[0] = c * rdet;
     F.Li[1] = -b * rdet;
     F.Li[2] = a * rdet;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const real m0 = lm.Mh[j], m1 = lm.Mk[j];
-      F.Z[0][j] = F.Li[0] * m0 + F.Li[1] * m1;
-      F.Z[1][j] = F.Li[1] * m0 + F.Li[2] * m1;
+      F.Z[0][j] = mad(F.Li[0], m0, F.Li[1] * m1);
+      F.Z[1][j] = mad(F.Li[1], m0, F.Li[2] * m1);
       F.Mh[j] = m0;
       F.Mk[j] = m1;
     }
   }
   const real* z0 = F.Z[0];
   const real* z1 = F.Z[1];
-  const real t[6] = {lm.Mh[0] * z0[0] + lm.Mk[0] * z1[0], lm.Mh[1] * z0[0] + lm.Mk[1] * z1[0],
-                     lm.Mh[1] * z0[1] + lm.Mk[1] * z1[1], lm.Mh[2] * z0[0] + lm.Mk[2] * z1[0],
-                     lm.Mh[2] * z0[1] + lm.Mk[2] * z1[1], lm.Mh[2] * z0[2] + lm.Mk[2] * z1[2]};
+  const real t[6] = {mad(lm.Mh[0], z0[0], lm.Mk[0] * z1[0]), mad(lm.Mh[1], z0[0], lm.Mk[1] * z1[0]),
+                     mad(lm.Mh[1], z0[1], lm.Mk[1] * z1[1]), mad(lm.Mh[2], z0[0], lm.Mk[2] * z1[0]),
+                     mad(lm.Mh[2], z0[1], lm.Mk[2] * z1[1]), mad(lm.Mh[2], z0[2], lm.Mk[2] * z1[2])};
   real s[6] = {M00, M10, M11, M20, M21, M22};  // s00, s10, s11, s20, s21, s22
 #pragma unroll
   for (int e = 0; e < 6; ++e) s[e] -= pair_sum(t[e]);  // minus front + back (arrow_factor)
   {
     const real s00 = s[0], s10 = s[1], s11 = s[2], s20 = s[3], s21 = s[4], s22 = s[5];
-    const real c00 = s11 * s22 - s21 * s21;
-    const real c10 = s21 * s20 - s10 * s22;
-    const real c20 = s10 * s21 - s11 * s20;
-    const real rdet = real(1.0) / (s00 * c00 + s10 * c10 + s20 * c20);
+    const real c00 = mad(s11, s22, -(s21 * s21));
+    const real c10 = mad(s21, s20, -(s10 * s22));
+    const real c20 = mad(s10, s21, -(s11 * s20));
+    const real rdet = real(1.0) / mad(s20, c20, mad(s10, c10, s00 * c00));
     F.Si[0] = c00 * rdet;
     F.Si[1] = c10 * rdet;
-    F.Si[2] = (s00 * s22 - s20 * s20) * rdet;
+    F.Si[2] = mad(s00, s22, -(s20 * s20)) * rdet;
     F.Si[3] = c20 * rdet;
-    F.Si[4] = (s20 * s10 - s00 * s21) * rdet;
-    F.Si[5] = (s00 * s11 - s10 * s10) * rdet;
+    F.Si[4] = mad(s20, s10, -(s00 * s21)) * rdet;
+    F.Si[5] = mad(s00, s11, -(s10 * s10)) * rdet;
   }
   // unconstrained accelerations: M v = S'u - h
   real vb[3], vl[2];
@@ -307,17 +307,17 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
     real r0 = -jd0, r1 = -jd1;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
-      A00 += J[0][i] * Y[0][i];
-      A01 += J[0][i] * Y[1][i];
-      A11 += J[1][i] * Y[1][i];
-      r0 -= J[0][i] * v[i];
-      r1 -= J[1][i] * v[i];
+      A00 = mad(J[0][i], Y[0][i], A00);
+      A01 = mad(J[0][i], Y[1][i], A01);
+      A11 = mad(J[1][i], Y[1][i], A11);
+      r0 = mad(-J[0][i], v[i], r0);
+      r1 = mad(-J[1][i], v[i], r1);
     }
-    const real rdet = real(1.0) / (A00 * A11 - A01 * A01);
-    const real lam0 = (A11 * r0 - A01 * r1) * rdet;
-    const real lam1 = (A00 * r1 - A01 * r0) * rdet;
+    const real rdet = real(1.0) / mad(A00, A11, -(A01 * A01));
+    const real lam0 = mad(A11, r0, -(A01 * r1)) * rdet;
+    const real lam1 = mad(A00, r1, -(A01 * r0)) * rdet;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) v[i] += Y[0][i] * lam0 + Y[1][i] * lam1;
+    for (int i = 0; i < 7; ++i) v[i] += mad(Y[0][i], lam0, Y[1][i] * lam1);
     y[sback ? 2 : 0] = lam0;
     y[sback ? 3 : 1] = lam1;
   }

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=${1:-q}
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_variants.py tests/test_gpu_solve.py -x -q --timeout 200 --timeout-method thread > gpurun_out/quick_${TAG}.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/quick_${TAG}.log | head -20; tail -5 gpurun_out/quick_${TAG}.log; exit 1; }
+timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_kernels.py tests/test_gpu_variants.py tests/test_gpu_solve.py} -x -q --timeout 200 --timeout-method thread > gpurun_out/quick_${TAG}.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/quick_${TAG}.log | head -20; tail -5 gpurun_out/quick_${TAG}.log; exit 1; }
 tail -1 gpurun_out/quick_${TAG}.log
 for b in ${BATCHES:-1024 4096}; do
   timeout -k 10 200 python bench.py --steps 6 --warmup 2 --batch-per-gpu $b --no-cpu-baseline > gpurun_out/q.json 2>gpurun_out/q.err || { tail gpurun_out/q.err; exit 1; }
