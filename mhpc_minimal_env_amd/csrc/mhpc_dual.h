@@ -80,6 +80,8 @@ MHPC_HD Dual mad(Dual a, real b, real c) { return Dual(fma(a.v, b, c), a.d * b);
 // Scalar-generic elementary functions (real and Dual share the model source).
 MHPC_HD real val(real a) { return a; }
 MHPC_HD real val(Dual a) { return a.v; }
+MHPC_HD real tangent(real) { return real(0.0); }
+MHPC_HD real tangent(Dual a) { return a.d; }
 
 #ifndef MHPC_FP32
 // sin and cos of a link angle: one Cody-Waite reduction by pi/2 (two-part pi/2, FMA) and

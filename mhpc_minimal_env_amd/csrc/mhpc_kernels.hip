@@ -9,9 +9,10 @@
 //              Armijo trials of forward_iteration (LS) at once, each lane a serial
 //              multi-phase rollout with costs, barrier, AL and phase transitions; the
 //              first accepted trial is selected in-wave (MultiPhaseDDP.cpp:130-151).
-//   k_partials lane = (problem, knot, tangent direction): dual-number evaluation of the
-//              whole-body model -> every column of A,B,C,D and of the impact Jacobian Px
-//              in parallel (forward_sweep_partials_only, SinglePhase.cpp:147-180).
+//   k_partials lane = (problem, WB knot, direction group): the knot's forward dynamics once,
+//              then every column of A,B,C,D by implicit differentiation of the contact KKT
+//              system (forward_sweep_partials_only, SinglePhase.cpp:147-180); the impact
+//              Jacobian Px by dual numbers (k_partials_impact).
 //   k_bws      one wavefront per problem: the backward Riccati sweep over all phases with
 //              impact-aware steps and the regularisation-retry loop
 //              (MultiPhaseDDP.cpp:100-127,196-241, SinglePhase.cpp:183-216,
@@ -770,86 +771,107 @@ hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, in
 }
 
 // ============================================================================================
-// k_partials: one lane per (problem, knot, tangent direction)
+// k_partials: forward_sweep_partials_only (SinglePhase.cpp:147-180) -- the dynamics
+// Jacobians of every WB knot of the nominal, by implicit differentiation of the contact KKT
+// system at the knot's solution (mhpc_model.h, WbKnot): the lane solves the knot's forward
+// dynamics once and then, per tangent direction, evaluates the inverse-dynamics residual in
+// dual numbers and solves with the knot's own factorisation.  Two launches over the knot
+// grid, a lane per (problem, WB knot) each: G = 0 the configuration directions 2..6 (plus
+// the knot's control / force cost derivatives), G = 1 the velocity directions 9..13 and the
+// controls 14..17; directions 0, 1, 7, 8 (base position / velocity) are exact zeros written
+// once at create.  k_partials_impact: the impact Jacobian Px at the end of the touchdown
+// phases, one lane per (problem, impact, direction), dual numbers through wb_impact.
 // ============================================================================================
-// Two launches with their own register allocation: VC = false takes the configuration
-// directions (full dual arithmetic, 7 per knot) and the impact Jacobian, VC = true the
-// velocity / control directions (11 per knot), where M, its factorisation and the
-// Jacobians stay plain doubles -- their derivative is exactly zero there.
-#ifndef MHPC_PAR_WAVES
-#define MHPC_PAR_WAVES 1
+// Direction groups, one launch each: [d0, d1) of the record's 18 columns (the controls'
+// columns need no residual, just a solve).  MHPC_PAR_GROUPS = 4 splits both groups in two
+// (more lanes, each with a shorter chain; the knot's forward dynamics is repeated per group).
+#ifndef MHPC_PAR_GROUPS
+#define MHPC_PAR_GROUPS 2
 #endif
-#ifndef MHPC_PARV_WAVES
-#define MHPC_PARV_WAVES 1
-#endif
-template <bool VC>
-__global__ __launch_bounds__(256, VC ? MHPC_PARV_WAVES : MHPC_PAR_WAVES) void k_partials(
-    SolveParams sp, DevBufs d) {
-  const int items = VC ? sp.par_items_v : sp.par_items;
-  const int* off = VC ? sp.par_v_off : sp.par_item_off;
+constexpr int kParGroups = MHPC_PAR_GROUPS;
+constexpr int kParD0[4] = {2, kParGroups == 4 ? 5 : 9, 9, 14};
+constexpr int kParD1[4] = {kParGroups == 4 ? 5 : 7, kParGroups == 4 ? 7 : 18, 14, 18};
+
+template <int SF, int G>
+__device__ __forceinline__ void partials_knot(const real* nk, real* rec) {
+  constexpr int d0 = kParD0[G], d1 = kParD1[G];
+  real x[14], u[4];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) x[i] = nk[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = nk[14 + i];
+  WbKnot K;
+  wb_knot_primal<SF>(x, u, K);
+#pragma unroll 1
+  for (int dir = d0; dir < (d1 < 7 ? d1 : 7); ++dir) {
+    real o[9];
+    wb_knot_partial_q<SF>(x, K, dir, o);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+  }
+#pragma unroll 1
+  for (int dir = d0 > 9 ? d0 : 9; dir < (d1 < 14 ? d1 : 14); ++dir) {
+    real o[9];
+    wb_knot_partial_qd<SF>(x, K, dir, o);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+  }
+#pragma unroll 1
+  for (int dir = d0 > 14 ? d0 : 14; dir < d1; ++dir) {
+    real o[9];
+    wb_knot_partial_u<SF>(K, dir, o);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = (int)(t / items);
+  const int b = (int)(t / sp.par_knots);
   if (b >= sp.B) return;
-  const int it = (int)(t - (long)b * items);
+  const int it = (int)(t - (long)b * sp.par_knots);
   const ProbState* st = &d.st[b];
   if (!(st->active && st->ddp_active)) return;
   int p = 0;
-  while (it >= off[p + 1]) ++p;
-  const int loc = it - off[p];
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const int nom = st->nom_slot;
-  // The planar model is invariant to the base position (x, z) and its velocity (xdot,
-  // zdot): the columns of directions 0, 1, 7, 8 are exact zeros (the reference's CasADi
-  // Jacobians carry them as structural zeros), written once when the buffer is created, so
-  // only 5 configuration and 9 velocity / control directions per knot get a lane.
-  if (VC || loc < (N - 1) * PAR_QD) {
-    const int k = VC ? loc / PAR_VD : loc / PAR_QD;
-    const int dir = VC ? 9 + (loc - k * PAR_VD) : 2 + (loc - k * PAR_QD);
-    const real* nk = traj_ptr(sp, d, b, nom, ko + k);
-    Dual u[4], f[14], y[4];
+  while (it >= sp.par_knot_off[p + 1]) ++p;
+  const int k = it - sp.par_knot_off[p];
+  const int ko = sp.ko[p], mode = sp.mode[p];
+  const real* nk = traj_ptr(sp, d, b, st->nom_slot, ko + k);
+  real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+  if (mode == 1) partials_knot<kBack, G>(nk, rec);
+  else if (mode == 3) partials_knot<kFront, G>(nk, rec);
+  else partials_knot<-1, G>(nk, rec);
+  if (G == 0) {
+    // running-cost derivatives of controls and contact forces at the nominal knot
+    // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
+    real c[14];
+    wb_cost_uy_derivs(mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
+                      st->eps_tq[p], st->eps_grf[p], c);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = Dual(nk[14 + i], 14 + i == dir ? real(1.0) : real(0.0));
-    if (!VC) {
-      Dual x[14];
-#pragma unroll
-      for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
-      wb_dynamics<Dual>(x, u, mode, f, y);
-    } else {
-      real xq[7];
-      Dual xv[7];
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        xq[i] = nk[i];
-        xv[i] = Dual(nk[7 + i], 7 + i == dir ? real(1.0) : real(0.0));
-      }
-      wb_dynamics_qv<real, Dual>(xq, xv, u, mode, f, y);
-    }
-    real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-    real* out = rec + dir * 9;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) out[i] = f[7 + i].d;
-    out[7] = mode == 1 ? y[2].d : y[0].d;
-    out[8] = mode == 1 ? y[3].d : y[1].d;
-    if (!VC && dir == 2) {
-      // running-cost derivatives of controls and contact forces at the nominal knot
-      // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
-      real c[14];
-      wb_cost_uy_derivs(mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
-                        st->eps_tq[p], st->eps_grf[p], c);
-#pragma unroll
-      for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
-    }
-  } else {
-    const int dir = loc - (N - 1) * PAR_QD;
-    const real* nk = traj_ptr(sp, d, b, nom, ko + N - 1);
-    Dual x[14], xp[14], lam[2];
-#pragma unroll
-    for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
-    wb_impact<Dual>(x, mode == 2 ? kFront : kBack, xp, lam);
-    real* out = d.px + ((size_t)b * MAXP + p) * 196 + dir * 14;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) out[i] = xp[i].d;
+    for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
   }
+}
+
+__global__ __launch_bounds__(256) void k_partials_impact(SolveParams sp, DevBufs d) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = (int)(t / sp.par_imp);
+  if (b >= sp.B) return;
+  const int it = (int)(t - (long)b * sp.par_imp);
+  const ProbState* st = &d.st[b];
+  if (!(st->active && st->ddp_active)) return;
+  int p = 0;
+  while (it >= sp.par_imp_off[p + 1]) ++p;
+  const int dir = it - sp.par_imp_off[p];
+  const int mode = sp.mode[p];
+  const real* nk = traj_ptr(sp, d, b, st->nom_slot, sp.ko[p] + sp.N[p] - 1);
+  Dual x[14], xp[14], lam[2];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
+  wb_impact<Dual>(x, mode == 2 ? kFront : kBack, xp, lam);
+  real* out = d.px + ((size_t)b * MAXP + p) * 196 + dir * 14;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) out[i] = xp[i].d;
 }
 
 // ============================================================================================
@@ -1167,16 +1189,15 @@ __global__ void k_eval_wb_par(int n, int mode, const real* x, const real* u, rea
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * 18) return;
   const int i = t / 18, dir = t % 18;
-  Dual xx[14], uu[4], f[14], y[4];
-  for (int a = 0; a < 14; ++a) xx[a] = Dual(x[(size_t)i * 14 + a], a == dir ? real(1.0) : real(0.0));
-  for (int a = 0; a < 4; ++a) uu[a] = Dual(u[(size_t)i * 4 + a], 14 + a == dir ? real(1.0) : real(0.0));
-  wb_dynamics<Dual>(xx, uu, mode, f, y);
+  // the partials kernel's method (implicit differentiation at the point's solution)
+  real a[14], c[4];
+  wb_partial_column(x + (size_t)i * 14, u + (size_t)i * 4, mode, dir, a, c);
   if (dir < 14) {
-    for (int r = 0; r < 14; ++r) Ac[(size_t)i * 196 + r * 14 + dir] = f[r].d;
-    for (int r = 0; r < 4; ++r) C[(size_t)i * 56 + r * 14 + dir] = y[r].d;
+    for (int r = 0; r < 14; ++r) Ac[(size_t)i * 196 + r * 14 + dir] = a[r];
+    for (int r = 0; r < 4; ++r) C[(size_t)i * 56 + r * 14 + dir] = c[r];
   } else {
-    for (int r = 0; r < 14; ++r) Bc[(size_t)i * 56 + r * 4 + dir - 14] = f[r].d;
-    for (int r = 0; r < 4; ++r) D[(size_t)i * 16 + r * 4 + dir - 14] = y[r].d;
+    for (int r = 0; r < 14; ++r) Bc[(size_t)i * 56 + r * 4 + dir - 14] = a[r];
+    for (int r = 0; r < 4; ++r) D[(size_t)i * 16 + r * 4 + dir - 14] = c[r];
   }
 }
 
@@ -1331,11 +1352,18 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real
   return hipGetLastError();
 }
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  const long tq = (long)sp.B * sp.par_items, tv = (long)sp.B * sp.par_items_v;
-  if (tq > 0)
-    hipLaunchKernelGGL(k_partials<false>, dim3((unsigned)((tq + 255) / 256)), dim3(256), 0, s, sp, d);
-  if (tv > 0)
-    hipLaunchKernelGGL(k_partials<true>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, sp, d);
+  const long tk = (long)sp.B * sp.par_knots, ti = (long)sp.B * sp.par_imp;
+  if (tk > 0) {
+    const dim3 grid((unsigned)((tk + 255) / 256));
+    hipLaunchKernelGGL(k_partials<0>, grid, dim3(256), 0, s, sp, d);
+    hipLaunchKernelGGL(k_partials<1>, grid, dim3(256), 0, s, sp, d);
+    if (kParGroups == 4) {
+      hipLaunchKernelGGL(k_partials<2>, grid, dim3(256), 0, s, sp, d);
+      hipLaunchKernelGGL(k_partials<3>, grid, dim3(256), 0, s, sp, d);
+    }
+  }
+  if (ti > 0)
+    hipLaunchKernelGGL(k_partials_impact, dim3((unsigned)((ti + 255) / 256)), dim3(256), 0, s, sp, d);
   return hipGetLastError();
 }
 hipError_t launch_al_end(const SolveParams& sp, const DevBufs& d, int last, hipStream_t s) {

@@ -396,6 +396,276 @@ MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
   wb_dynamics_qv<S, S>(x, x + 7, u, mode, xdot, y);
 }
 
+// ---- Jacobians by implicit differentiation (the partials kernel, Dyn_*_par) --------------
+// The forward dynamics solve the contact KKT system
+//   R = M(q) qdd + h(q, qd) - S'u - J(q)' lam = 0,   C = J(q) qdd + Jd(q, qd) qd = 0
+// (C and lam only in stance).  Along a direction th of (q, qd, u), with qdd and lam held at
+// the knot's solution,  [M -J'; J 0] [dqdd; dlam] = -[R_th; C_th]:  one dual-number
+// evaluation of the residuals (inverse dynamics -- no factorisation, no division, the link
+// sines / cosines of the knot reused) and a solve with the knot's own factorisation, instead
+// of a dual-number evaluation of the whole forward dynamics per direction.  Same derivative
+// as forward-mode differentiation of wb_dynamics up to rounding.
+struct WbKnot {
+  WbGeo<real, real> g;
+  real M[28];              // packed mass matrix (the solves read its leg coupling rows)
+  ArrowFactor<real> AF;
+  real qdd[7], lam[2];
+  real J[2][7];            // stance foot Jacobian (stance only)
+  real A00, A01, A11, rdet;  // J M^-1 J' and 1 / its determinant (stance only)
+};
+
+// The knot's forward dynamics (wb_dynamics' arithmetic), keeping what the solves reuse.
+// SF: stance foot (kFront: mode 3, kBack: mode 1) or -1 (flight, modes 2 and 4).
+template <int SF>
+MHPC_HD void wb_knot_primal(const real* x, const real* u, WbKnot& K) {
+  MHPC_NO_FMA_WB
+  wb_geometry<real, real>(x, x + 7, K.g);
+  real h[7], v[7];
+  wb_mass_bias<real, real>(x + 7, K.g, K.M, h);
+  arrow_factor(K.M, K.AF);
+  v[0] = -h[0]; v[1] = -h[1]; v[2] = -h[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[3 + i] = u[i] - h[3 + i];
+  arrow_solve<real, real>(K.M, K.AF, v);
+  K.lam[0] = K.lam[1] = real(0.0);
+  if constexpr (SF >= 0) {
+    real jd[2];
+    wb_foot_jac_full<real, real, SF>(x + 7, K.g, K.J, jd);
+    real Y[2][7];  // M^-1 J'
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) Y[r][i] = K.J[r][i];
+      arrow_solve<real, real>(K.M, K.AF, Y[r]);
+    }
+    real A00 = real(0.0), A01 = real(0.0), A11 = real(0.0), r0 = -jd[0], r1 = -jd[1];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      A00 = mad(K.J[0][i], Y[0][i], A00);
+      A01 = mad(K.J[0][i], Y[1][i], A01);
+      A11 = mad(K.J[1][i], Y[1][i], A11);
+      r0 = mad(-K.J[0][i], v[i], r0);
+      r1 = mad(-K.J[1][i], v[i], r1);
+    }
+    K.A00 = A00; K.A01 = A01; K.A11 = A11;
+    K.rdet = real(1.0) / mad(A00, A11, -(A01 * A01));
+    K.lam[0] = mad(A11, r0, -(A01 * r1)) * K.rdet;
+    K.lam[1] = mad(A00, r1, -(A01 * r0)) * K.rdet;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) v[i] += mad(Y[0][i], K.lam[0], Y[1][i] * K.lam[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) K.qdd[i] = v[i];
+}
+
+// [M -J'; J 0] [v; lam] = [rhs; -c] with the knot's factorisation (rhs in v on entry);
+// out = (v 7, lam 2) -- one column of the partials record.  The contact correction
+// M^-1 J' lam is a second arrow solve rather than M^-1 J' kept per knot (14 fewer live
+// doubles per lane).
+template <int SF>
+MHPC_HD void wb_knot_solve(const WbKnot& K, real v[7], real c0, real c1, real out[9]) {
+  MHPC_NO_FMA_WB
+  arrow_solve<real, real>(K.M, K.AF, v);
+  real l0 = real(0.0), l1 = real(0.0);
+  if constexpr (SF >= 0) {
+    real r0 = -c0, r1 = -c1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      r0 = mad(-K.J[0][i], v[i], r0);
+      r1 = mad(-K.J[1][i], v[i], r1);
+    }
+    l0 = mad(K.A11, r0, -(K.A01 * r1)) * K.rdet;
+    l1 = mad(K.A00, r1, -(K.A01 * r0)) * K.rdet;
+    real w[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[i] = mad(K.J[0][i], l0, K.J[1][i] * l1);
+    arrow_solve<real, real>(K.M, K.AF, w);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) v[i] += w[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) out[i] = v[i];
+  out[7] = l0;
+  out[8] = l1;
+}
+
+// Inverse dynamics of leg F's thigh and shank at the fixed qdd: adds
+// m Jc'(Jc qdd + Jcdot qd + g) + Ic w (w . qdd) of each body to R (add_leg's M qdd + h).
+template <class Q, class V, int F>
+MHPC_HD void id_leg(const V* xv, const WbGeo<Q, V>& g, const real* qdd, V R[7]) {
+  MHPC_NO_FMA_WB
+  constexpr real sg = F == kFront ? real(1.0) : -real(1.0);
+  constexpr int idx[5] = {0, 1, 2, 3 + 2 * F, 4 + 2 * F};
+  const V thd2 = xv[2] * xv[2];
+  const V hax = (-sg * kHipX) * g.cth * thd2;
+  const V haz = (sg * kHipX) * g.sth * thd2;
+  const real al1 = qdd[2] + qdd[idx[3]];  // angular accelerations of thigh and shank
+  const real al2 = al1 + qdd[idx[4]];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    Q jx[5], jz[5];
+    V jdx, jdz;
+    real m, ic;
+    if (b == 0) {
+      leg_point_jac<Q, V, F>(g, kThighCom, real(0.0), jx, jz, &jdx, &jdz);
+      m = kThighMass; ic = kThighInertiaCom;
+    } else {
+      leg_point_jac<Q, V, F>(g, kThighLen, kShankCom, jx, jz, &jdx, &jdz);
+      m = kShankMass; ic = kShankInertiaCom;
+    }
+    const int nc = b == 0 ? 4 : 5;
+    // CoM acceleration (x/z columns of Jc are unit vectors)
+    V ax = (jdx + hax) + qdd[0], az = ((jdz + haz) + kGrav) + qdd[1];
+#pragma unroll
+    for (int a = 2; a < 5; ++a) {
+      if (a >= nc) continue;
+      ax = mad(jx[a], qdd[idx[a]], ax);
+      az = mad(jz[a], qdd[idx[a]], az);
+    }
+    const real ia = ic * (b == 0 ? al1 : al2);
+    R[0] += m * ax;
+    R[1] += m * az;
+#pragma unroll
+    for (int a = 2; a < 5; ++a) {
+      if (a >= nc) continue;
+      R[idx[a]] += m * mad(jx[a], ax, jz[a] * az) + ia;
+    }
+  }
+}
+
+// Tangents of R and C along one direction, given the link geometry g in (Q, V) (the body
+// terms of M qdd + h and the stance foot's J' lam, C = J qdd + Jd qd; the constant base
+// terms and S'u carry no tangent).
+template <class Q, class V, int SF>
+MHPC_HD void wb_residual_tangent(const V* xv, const WbGeo<Q, V>& g, const WbKnot& K, real rhs[7],
+                                 real* c0, real* c1) {
+  MHPC_NO_FMA_WB
+  V R[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) R[i] = V(real(0.0));
+  id_leg<Q, V, kFront>(xv, g, K.qdd, R);
+  id_leg<Q, V, kBack>(xv, g, K.qdd, R);
+  *c0 = *c1 = real(0.0);
+  if constexpr (SF >= 0) {
+    Q jx[5], jz[5];
+    V jdx, jdz;
+    leg_point_jac<Q, V, SF>(g, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
+    constexpr real sg = SF == kFront ? real(1.0) : -real(1.0);
+    constexpr int idx[5] = {0, 1, 2, 3 + 2 * SF, 4 + 2 * SF};
+    const V thd2 = xv[2] * xv[2];
+    V C0 = jdx + (-sg * kHipX) * g.cth * thd2;
+    V C1 = jdz + (sg * kHipX) * g.sth * thd2;
+    C0 = C0 + K.qdd[0];
+    C1 = C1 + K.qdd[1];
+#pragma unroll
+    for (int a = 2; a < 5; ++a) {
+      C0 = mad(jx[a], K.qdd[idx[a]], C0);
+      C1 = mad(jz[a], K.qdd[idx[a]], C1);
+    }
+    R[0] -= V(K.lam[0]);
+    R[1] -= V(K.lam[1]);
+#pragma unroll
+    for (int a = 2; a < 5; ++a) R[idx[a]] -= mad(jx[a], K.lam[0], jz[a] * K.lam[1]);
+    *c0 = tangent(C0);
+    *c1 = tangent(C1);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) rhs[i] = -tangent(R[i]);
+}
+
+// Column dir of the continuous Jacobians: d qdd (7) and d lam (2) of the stance foot.
+// q directions (dir 0..6): dual geometry from the knot's sines / cosines.
+template <int SF>
+MHPC_HD void wb_knot_partial_q(const real* x, const WbKnot& K, int dir, real out[9]) {
+  MHPC_NO_FMA_WB
+  real rhs[7], c0, c1;
+  const real dth = dir == 2 ? real(1.0) : real(0.0);
+  WbGeo<Dual, Dual> g;
+  g.sth = Dual(K.g.sth, K.g.cth * dth);
+  g.cth = Dual(K.g.cth, -K.g.sth * dth);
+  Dual xv[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) xv[i] = Dual(x[7 + i]);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+    const real d1 = dth + (dir == ih ? real(1.0) : real(0.0));
+    const real d2 = d1 + (dir == ik ? real(1.0) : real(0.0));
+    const LegGeo<real, real>& P = K.g.leg[f];
+    g.leg[f].s1 = Dual(P.s1, P.c1 * d1);
+    g.leg[f].c1 = Dual(P.c1, -P.s1 * d1);
+    g.leg[f].s2 = Dual(P.s2, P.c2 * d2);
+    g.leg[f].c2 = Dual(P.c2, -P.s2 * d2);
+    g.leg[f].w1 = Dual(P.w1);
+    g.leg[f].w2 = Dual(P.w2);
+  }
+  wb_residual_tangent<Dual, Dual, SF>(xv, g, K, rhs, &c0, &c1);
+  wb_knot_solve<SF>(K, rhs, c0, c1, out);
+}
+// qd directions (dir 7..13): only the link rates carry a tangent (M, J: none).
+template <int SF>
+MHPC_HD void wb_knot_partial_qd(const real* x, const WbKnot& K, int dir, real out[9]) {
+  MHPC_NO_FMA_WB
+  real rhs[7], c0, c1;
+  Dual xv[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) xv[i] = Dual(x[7 + i], 7 + i == dir ? real(1.0) : real(0.0));
+  WbGeo<real, Dual> g;
+  g.sth = K.g.sth;
+  g.cth = K.g.cth;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+    g.leg[f].s1 = K.g.leg[f].s1; g.leg[f].c1 = K.g.leg[f].c1;
+    g.leg[f].s2 = K.g.leg[f].s2; g.leg[f].c2 = K.g.leg[f].c2;
+    g.leg[f].w1 = xv[2] + xv[ih];
+    g.leg[f].w2 = g.leg[f].w1 + xv[ik];
+  }
+  wb_residual_tangent<real, Dual, SF>(xv, g, K, rhs, &c0, &c1);
+  wb_knot_solve<SF>(K, rhs, c0, c1, out);
+}
+// u directions (dir 14..17): rhs = S'e, no constraint tangent.
+template <int SF>
+MHPC_HD void wb_knot_partial_u(const WbKnot& K, int dir, real out[9]) {
+  real rhs[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) rhs[i] = 3 + (dir - 14) == i ? real(1.0) : real(0.0);
+  wb_knot_solve<SF>(K, rhs, real(0.0), real(0.0), out);
+}
+template <int SF>
+MHPC_HD void wb_knot_partial(const real* x, const WbKnot& K, int dir, real out[9]) {
+  if (dir < 7) wb_knot_partial_q<SF>(x, K, dir, out);
+  else if (dir < 14) wb_knot_partial_qd<SF>(x, K, dir, out);
+  else wb_knot_partial_u<SF>(K, dir, out);
+}
+
+// One column (dir 0..13: Ac / C, 14..17: Bc / D) of the dense continuous Jacobians of
+// Dyn_*_par by implicit differentiation: a (14 rows: the qd rows of xdot = (qd, qdd), then
+// d qdd), c (4 rows of y, the stance foot's two).  For the eval hooks and host checks; the
+// partials kernel writes the record directly.
+template <int SF>
+MHPC_HD void wb_partial_column_sf(const real* x, const real* u, int dir, real a[14], real c[4]) {
+  WbKnot K;
+  wb_knot_primal<SF>(x, u, K);
+  real o[9];
+  wb_knot_partial<SF>(x, K, dir, o);
+  for (int i = 0; i < 7; ++i) {
+    a[i] = dir == 7 + i ? real(1.0) : real(0.0);
+    a[7 + i] = o[i];
+  }
+  for (int i = 0; i < 4; ++i) c[i] = real(0.0);
+  if (SF >= 0) {
+    c[2 * SF] = o[7];
+    c[2 * SF + 1] = o[8];
+  }
+}
+MHPC_HD void wb_partial_column(const real* x, const real* u, int mode, int dir, real a[14],
+                               real c[4]) {
+  if (mode == 1) wb_partial_column_sf<kBack>(x, u, dir, a, c);
+  else if (mode == 3) wb_partial_column_sf<kFront>(x, u, dir, a, c);
+  else wb_partial_column_sf<-1>(x, u, dir, a, c);
+}
+
 // Plastic impact of foot F (Imp_F: front, end of mode 2; Imp_B: back, end of mode 4):
 // q+ = q, [M -J'; J 0][qd+; Lam] = [M qd-; 0].
 template <class S, int F>

@@ -127,19 +127,19 @@ static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
     sp.xs[p] = wb ? 14 : 6;
     sp.dt[p] = wb ? desc.dt_wb : desc.dt_fb;
     ko += desc.N[p];
-    sp.par_item_off[p] = items;
-    sp.par_v_off[p] = items_v;
+    sp.par_knot_off[p] = items;
+    sp.par_imp_off[p] = items_v;
     if (wb) {
-      items += (desc.N[p] - 1) * PAR_QD + ((sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0);
-      items_v += (desc.N[p] - 1) * PAR_VD;
+      items += desc.N[p] - 1;
+      items_v += (sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0;
     }
   }
   for (int p = sp.P; p <= MAXP; ++p) {
-    sp.par_item_off[p] = items;
-    sp.par_v_off[p] = items_v;
+    sp.par_knot_off[p] = items;
+    sp.par_imp_off[p] = items_v;
   }
-  sp.par_items = items;
-  sp.par_items_v = items_v;
+  sp.par_knots = items;
+  sp.par_imp = items_v;
   sp.NK = ko;
 }
 

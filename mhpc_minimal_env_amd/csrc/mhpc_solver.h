@@ -29,8 +29,6 @@ constexpr int KS = 24;        // doubles per knot record in traj
 constexpr int PS_JAC = 162;   // 18 tangent directions x (7 qddot + 2 contact-force rows)
 constexpr int PS = 176;       // doubles per knot in par: Jacobians + 14 cost derivatives
                               // (lu 4, luu 4, ly 2, lyy 4 of the stance block)
-constexpr int PAR_QD = 5;      // partials lanes per WB knot: configuration directions 2..6
-constexpr int PAR_VD = 9;      // velocity / control directions 9..17 (0, 1, 7, 8: exact zeros)
 constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
 constexpr int TRACE = MHPC_TRACE_LEN;
@@ -57,10 +55,10 @@ struct SolveParams {
   real eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
   int AL_active, ReB_active;
   int buf[MAXP];             // phase buffer of each phase (receding horizon, see k_store_*)
-  // partials work items per problem and their prefix offsets per phase, in two classes:
-  // configuration directions (+ the impact directions) and velocity / control directions
-  int par_items, par_items_v;
-  int par_item_off[MAXP + 1], par_v_off[MAXP + 1];
+  // partials work per problem and its prefix offsets per phase: WB knots with Jacobians
+  // (N - 1 per WB phase) and impact directions (14 per touchdown phase)
+  int par_knots, par_imp;
+  int par_knot_off[MAXP + 1], par_imp_off[MAXP + 1];
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
   int ncu, var_bws, var_ro, var_overlap;

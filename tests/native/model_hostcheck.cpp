@@ -29,6 +29,18 @@ void hc_wb_partials(const double* x, const double* u, int mode, double* Ac, doub
   }
 }
 
+// The same matrices by implicit differentiation of the KKT system (wb_partial_column: what
+// the partials kernel computes).
+void hc_wb_partials_ift(const double* x, const double* u, int mode, double* Ac, double* Bc,
+                        double* C, double* D) {
+  for (int j = 0; j < 18; ++j) {
+    double a[14], c[4];
+    wb_partial_column(x, u, mode, j, a, c);
+    for (int i = 0; i < 14; ++i) (j < 14 ? Ac[i + 14 * j] : Bc[i + 14 * (j - 14)]) = a[i];
+    for (int i = 0; i < 4; ++i) (j < 14 ? C[i + 4 * j] : D[i + 4 * (j - 14)]) = c[i];
+  }
+}
+
 void hc_wb_impact(const double* x, int foot, double* xp, double* lam) {
   wb_impact<double>(x, foot, xp, lam);
 }

@@ -46,6 +46,25 @@ def test_dynamics_and_jacobians(hc, kat, mode, name):
         assert rel_err(D.reshape(4, 4, order="F"), kat[name + "_par.D"][i]) < KAT_TOL["jac"]
 
 
+@pytest.mark.parametrize("mode,name", [(1, "Dyn_BS"), (2, "Dyn_FL"), (3, "Dyn_FS"), (4, "Dyn_FL")])
+def test_jacobians_by_implicit_differentiation(hc, kat, mode, name):
+    """The partials kernel's method (implicit differentiation of the KKT system at the
+    knot's solution, wb_partial_column) vs the reference's CasADi Jacobians and vs
+    forward-mode dual numbers through the whole forward dynamics (the same derivative)."""
+    x, u = kat["x"], kat["u"]
+    worst = 0.0
+    for i in range(len(x)):
+        A, B, C, D = np.zeros(196), np.zeros(56), np.zeros(56), np.zeros(16)
+        hc.hc_wb_partials_ift(P(x[i]), P(u[i]), mode, P(A), P(B), P(C), P(D))
+        A2, B2, C2, D2 = np.zeros(196), np.zeros(56), np.zeros(56), np.zeros(16)
+        hc.hc_wb_partials(P(x[i]), P(u[i]), mode, P(A2), P(B2), P(C2), P(D2))
+        for m, m2, key, shape in ((A, A2, "Ac", (14, 14)), (B, B2, "Bc", (14, 4)),
+                                  (C, C2, "C", (4, 14)), (D, D2, "D", (4, 4))):
+            assert rel_err(m.reshape(shape, order="F"), kat[f"{name}_par.{key}"][i]) < KAT_TOL["jac"]
+            worst = max(worst, rel_err(m, m2))
+    assert worst < 1e-10, worst
+
+
 @pytest.mark.parametrize("foot,name", [(0, "Imp_F"), (1, "Imp_B")])
 def test_impact(hc, kat, foot, name):
     for i, x in enumerate(kat["x"]):

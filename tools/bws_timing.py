@@ -16,6 +16,8 @@ dbg = lib.mhpc_dbg_bws_cycles
 dbg.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 desc = configs.c3_desc()
 loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=B, device=0)
+# the round marks sit in the whole-sweep kernel (PART 0): no split at the WB / SRB boundary
+loco.set_kernel_variant(overlap="off")
 loco.set_initial_condition(configs.x0_for(desc, B))
 buf = (ctypes.c_ulonglong * 12)()
 for it in range(2):
