@@ -342,7 +342,8 @@ def run_sweep(args, torch):
             "solve_only_per_s": B * args.steps / (solve_ms / 1e3) if solve_ms > 0 else None,
             "ddp_iters_per_s": ddp / dt, "steps": args.steps, "warmup": args.warmup,
             "dtype": "f32" if args.workload == "c5f32" else "f64",
-            "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in stats.items()},
+            "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
+            "profiled_steps": prof_steps,
             "roofline": roofline_of(stats, B),
         }), flush=True)
         s.close()
@@ -377,6 +378,9 @@ def main():
                     help="pin the line-search launch variant (capi.RO_VARIANTS; tuning only)")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="partials beside the SRB half of the backward sweep (tuning only)")
+    ap.add_argument("--profile-steps", type=int, default=None,
+                    help="steps run after the timed region with per-launch HIP events (kernel "
+                         "times, roofline); default = --steps")
     ap.add_argument("--sub-batches", type=int, default=0,
                     help="concurrently scheduled sub-batches per GPU, 1..4 (0 = automatic; tuning only)")
     ap.add_argument("--batch-sweep", default=None,
@@ -423,8 +427,6 @@ def main():
                                                            args.sub_batches))
     for _ in range(args.warmup):
         s.step()
-    s.loco.set_profiling(True)
-    s.loco.reset_kernel_stats()
 
     def barrier():
         if dist is not None:
@@ -442,6 +444,15 @@ def main():
         ddp_iters += c["ddp_iters"]
     barrier()
     dt = time.perf_counter() - t0
+    # per-kernel HIP-event timing (an event pair around every launch) in separate steps after
+    # the timed region, so the events do not sit between the timed kernels
+    s.loco.set_profiling(True)
+    s.loco.reset_kernel_stats()
+    prof_steps = args.profile_steps if args.profile_steps is not None else args.steps
+    for _ in range(prof_steps):
+        s.step()
+    torch.cuda.synchronize()
+    s.loco.set_profiling(False)
 
     stats = s.loco.kernel_stats()
     tens = torch.tensor([dt, solve_ms / 1e3, float(ddp_iters)], dtype=torch.float64, device=tdev)
