@@ -210,6 +210,10 @@ void mhpc_destroy(mhpc_handle* h);
                                          so that one block's line search shares the chip with
                                          another block's sweep); 0 = automatic */
 #define MHPC_MAX_SUBBATCH 4
+#define MHPC_VARIANT_GRAPH 4          /* which: the solve's launch schedule as a HIP graph */
+#define MHPC_VARIANT_GRAPH_ON 1       /*   captured once per schedule, replayed */
+#define MHPC_VARIANT_GRAPH_OFF 2      /*   every launch issued from the host (default: the
+                                         replay measured no faster) */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

@@ -30,6 +30,8 @@ RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged"
 MHPC_VARIANT_OVERLAP = 2
 OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_VARIANT_SUBBATCH = 3
+MHPC_VARIANT_GRAPH = 4
+GRAPH_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_MAX_SUBBATCH = 4
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1

@@ -112,6 +112,12 @@ struct Handle {
   };
   std::vector<SubStreams> subs;
   hipEvent_t evstart = nullptr;
+  // the solve's launch schedule captured as a HIP graph (MHPC_VARIANT_GRAPH), replayed while
+  // the parameters it was captured with (launch arguments by value, schedule) are unchanged
+  int graph_req = 0;
+  hipGraphExec_t gexec = nullptr;
+  SolveParams gsp;
+  int gfull = -1, gnsub = -1;
 };
 
 // Phase layout of a descriptor: modes, knot counts and offsets, partials work items.
@@ -591,6 +597,44 @@ static int solve_async(Handle* h) {
   return MHPC_OK;
 }
 
+// The solve schedule as a HIP graph: ~35 dependent launches (two streams) replayed by the
+// device without a host round trip per launch.  Captured on first use and again whenever
+// the launch arguments (SolveParams by value), the schedule (real first rollout after
+// update_problem) or the sub-batch count change; not while per-launch profiling events are
+// requested (those need the host-issued schedule).
+static void drop_graph(Handle* h) {
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  h->gexec = nullptr;
+}
+static int solve_graph(Handle* h) {
+  const int nsub = sub_batches(h);
+  const bool same = h->gexec && h->gfull == (h->need_full ? 1 : 0) && h->gnsub == nsub &&
+                    memcmp(&h->gsp, &h->sp, sizeof(SolveParams)) == 0;
+  if (!same) {
+    drop_graph(h);
+    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    int rc = solve_async(h);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (ec != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("graph capture: ") + hipGetErrorString(ec));
+    const hipError_t ei = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+      h->gexec = nullptr;
+      return fail(MHPC_ERR_DEVICE, std::string("graph instantiate: ") + hipGetErrorString(ei));
+    }
+    memcpy(&h->gsp, &h->sp, sizeof(SolveParams));
+    h->gfull = h->need_full ? 1 : 0;
+    h->gnsub = nsub;
+  }
+  HIPCHK(hipGraphLaunch(h->gexec, h->stream));
+  return MHPC_OK;
+}
+
 int api_solve(Handle* h, int32_t* status) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
   if (!h->initialized) return fail(MHPC_ERR_STATE, "mhpc_initialize must precede mhpc_solve");
@@ -599,7 +643,12 @@ int api_solve(Handle* h, int32_t* status) {
     return fail(MHPC_ERR_STATE, "x0 changed: call mhpc_initialize or mhpc_update_problem first");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
-  int rc = solve_async(h);
+  // Off unless requested: replaying the schedule measured no faster than issuing it (the gaps
+  // between dependent kernels are device-side; profiles/r02_ab_graph.txt).  Never with
+  // sub-batches: a solve captured with their four-stream fan-out segfaulted on the host in
+  // the sub-batch parity test (sub-batching is off by default, profiles/r02_ab_subbatch.txt).
+  const bool graph = h->graph_req == MHPC_VARIANT_GRAPH_ON && !h->profile && sub_batches(h) <= 1;
+  int rc = graph ? solve_graph(h) : solve_async(h);
   if (rc) return rc;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   HIPCHK(hipMemcpyAsync(h->cnt, h->dcnt, NCNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -891,6 +940,11 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
     sp.var_overlap = variant;
     return MHPC_OK;
   }
+  if (which == MHPC_VARIANT_GRAPH) {
+    if (variant < 0 || variant > MHPC_VARIANT_GRAPH_OFF) return fail(MHPC_ERR_INVALID, "no such graph variant");
+    h->graph_req = variant;
+    return MHPC_OK;
+  }
   if (which == MHPC_VARIANT_SUBBATCH) {
     if (variant < 0 || variant > MHPC_MAX_SUBBATCH) return fail(MHPC_ERR_INVALID, "sub-batch count must be 0..4");
     h->nsub_req = variant;
@@ -926,6 +980,7 @@ void api_destroy(Handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  drop_graph(h);
   free_bufs(h);
   if (h->dcnt) (void)hipFree(h->dcnt);
   if (h->store) (void)hipFree(h->store);

@@ -344,13 +344,15 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
     def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto",
-                           sub_batches: int = 0):
+                           sub_batches: int = 0, graph: str = "auto"):
         """Pin the backward-sweep / line-search launch variant, the partials / sweep
-        overlap and the number of concurrently scheduled sub-batches
-        (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
+        overlap, the number of concurrently scheduled sub-batches and whether the solve
+        schedule replays as a HIP graph (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
         capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by batch size and phase layout."""
         L = capi.lib()
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SUBBATCH, int(sub_batches)),
+                   "mhpc_set_kernel_variant")
+        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_GRAPH, capi.GRAPH_VARIANTS[graph]),
                    "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_OVERLAP,
                                              capi.OVERLAP_VARIANTS[overlap]), "mhpc_set_kernel_variant")
