@@ -320,8 +320,6 @@ def run_sweep(args, torch):
                                                            args.sub_batches, args.graph))
         for _ in range(args.warmup):
             s.step()
-        s.loco.set_profiling(True)
-        s.loco.reset_kernel_stats()
         solve_ms = 0.0
         ddp = 0
         torch.cuda.synchronize()
@@ -333,6 +331,14 @@ def run_sweep(args, torch):
             ddp += c["ddp_iters"]
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        # per-kernel event timing in separate steps (see main)
+        s.loco.set_profiling(True)
+        s.loco.reset_kernel_stats()
+        prof_steps = args.profile_steps if args.profile_steps is not None else args.steps
+        for _ in range(prof_steps):
+            s.step()
+        torch.cuda.synchronize()
+        s.loco.set_profiling(False)
         stats = s.loco.kernel_stats()
         print(json.dumps({
             "metric": metric_of(args.workload), "batch": B, "value": B * args.steps / dt,
@@ -515,7 +521,8 @@ def main():
             },
             "ddp_iters_per_s": ddp_total / dt,
             "solve_only_per_s": total / solve_s if solve_s > 0 else None,
-            "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in stats.items()},
+            "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
+            "profiled_steps": prof_steps,
             "roofline": roofline_of(stats, B),
             "cpu_baseline": cpu if cpu is not None else {"value": None, "reason": why},
         }

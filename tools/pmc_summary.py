@@ -26,6 +26,9 @@ def load(path, counter):
             key = m.group(1) if m else name
             if key == "k_bws" and re.search(r"k_bws<\d+, \d+, 1>", name):
                 key = "k_bws_srb"  # SRB half of the split backward sweep
+            if key == "k_partials":  # one launch group: the two direction groups + impacts
+                g = re.search(r"k_partials<(\d+)>", name)
+                key = f"k_partials.g{g.group(1)}" if g else key
             acc[key].append(float(r["Counter_Value"]))
     return acc
 
@@ -43,6 +46,15 @@ def main():
         wb = sum(w) / len(w) * 1024
         res[k] = {"dispatches": len(f), "fetch_bytes_raw": fb, "write_bytes": wb,
                   "hbm_bytes_per_launch": 2 * fb + wb}
+    # the bench's k_partials launch = both direction-group kernels + the impact kernel
+    parts = [k for k in res if k.startswith("k_partials")]
+    if parts:
+        res["k_partials"] = {
+            "dispatches": min(res[k]["dispatches"] for k in parts),
+            "fetch_bytes_raw": sum(res[k]["fetch_bytes_raw"] for k in parts),
+            "write_bytes": sum(res[k]["write_bytes"] for k in parts),
+            "hbm_bytes_per_launch": sum(res[k]["hbm_bytes_per_launch"] for k in parts),
+            "sum_of": parts}
     doc = {"source": d, "note": note, "correction": "hbm = 2 * FETCH_SIZE*1024 + WRITE_SIZE*1024",
            "kernels": res}
     with open(out, "w") as fo:
