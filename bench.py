@@ -140,10 +140,13 @@ def cpu_sample_for(desc, opt, threads: int, seconds: float) -> int:
     return int(min(max(seconds / max(per, 1e-6), n), 131072))
 
 
-def load_pmc(kernel: str, batch: int):
+def load_pmc(kernel: str, batch: int, wl: str = "c3"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
-    batch size (profiles/pmc_traffic_b<batch>.json, tools/pmc_summary.py): (bytes, file)."""
-    path = os.path.join("profiles", f"pmc_traffic_b{batch}.json")
+    workload and batch size (profiles/pmc_traffic_b<batch>.json for C3,
+    profiles/pmc_traffic_<workload>_b<batch>.json otherwise; tools/pmc_summary.py):
+    (bytes, file), (None, None) when no such summary is committed."""
+    name = f"pmc_traffic_b{batch}.json" if wl == "c3" else f"pmc_traffic_{wl}_b{batch}.json"
+    path = os.path.join("profiles", name)
     if not os.path.exists(os.path.join(ROOT, path)):
         return None, None
     try:
@@ -154,7 +157,7 @@ def load_pmc(kernel: str, batch: int):
         return None, None
 
 
-def roofline_of(stats: dict, batch: int) -> dict:
+def roofline_of(stats: dict, batch: int, wl: str = "c3") -> dict:
     """HBM roofline of the kernel with the largest device time (+ its FP64 VALU rate in the
     reference's dense flop count, SURVEY.md 8d secondary roofline)."""
     dom = max(stats, key=lambda k: stats[k]["ms"])
@@ -163,7 +166,7 @@ def roofline_of(stats: dict, batch: int) -> dict:
     bytes_per_launch = ks["alg_bytes"] / max(ks["launches"], 1)
     flops_per_launch = ks.get("alg_flops", 0.0) / max(ks["launches"], 1)
     achieved = bytes_per_launch / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    traffic, src = load_pmc(dom, batch)
+    traffic, src = load_pmc(dom, batch, wl)
     r = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
          "traffic_source": src, "alg_bytes_per_launch": bytes_per_launch,
@@ -176,7 +179,7 @@ def roofline_of(stats: dict, batch: int) -> dict:
         t = v["ms"] / 1e3 / v["launches"]
         a = v["alg_bytes"] / v["launches"] / t / 1e9
         per[k.split("(")[0]] = {"avg_launch_ms": t * 1e3, "achieved": a, "frac": a / HBM_PEAK_GBS,
-                                "traffic": load_pmc(k, batch)[0]}
+                                "traffic": load_pmc(k, batch, wl)[0]}
     r["per_kernel"] = per
     if flops_per_launch > 0 and per_launch_s > 0:
         tf = flops_per_launch / per_launch_s / 1e12
@@ -350,7 +353,7 @@ def run_sweep(args, torch):
             "dtype": "f32" if args.workload == "c5f32" else "f64",
             "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
             "profiled_steps": prof_steps,
-            "roofline": roofline_of(stats, B),
+            "roofline": roofline_of(stats, B, args.workload),
         }), flush=True)
         s.close()
 
@@ -523,7 +526,7 @@ def main():
             "solve_only_per_s": total / solve_s if solve_s > 0 else None,
             "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
             "profiled_steps": prof_steps,
-            "roofline": roofline_of(stats, B),
+            "roofline": roofline_of(stats, B, args.workload),
             "cpu_baseline": cpu if cpu is not None else {"value": None, "reason": why},
         }
         if shard is not None:
