@@ -34,7 +34,25 @@ constexpr int QR = 24;          // rows of Q (padded)
 #ifndef MHPC_BWS_JTPAD
 #define MHPC_BWS_JTPAD 1
 #endif
-template <int NX> constexpr int JtStride = NX + MHPC_BWS_JTPAD;
+// Column-major blocks (MHPC_BWS_WT=1, default): the NQ dynamic rows of one column of [A B]
+// are contiguous in W (stride WR), the two stance rows of one column of [C D] in G2, and
+// the NQ entries Jt[row][NQ..NX-1] that R3 keeps in registers start 16-byte aligned (one
+// leading pad element per row), so R2 and R3 read their operand runs with ds_read_b128
+// (4 LDS cycles for 16 bytes per lane) instead of strided ds_read2_b64 pairs (8 cycles).
+// Jt row strides 18 / 10 doubles put the rows of a 16-lane b128 group on distinct banks
+// (tools/lds_bank_model.py).  Only the LDS layout changes: same products, same order.
+#ifndef MHPC_BWS_WT
+#define MHPC_BWS_WT 1
+#endif
+constexpr int WR = 8;  // column stride of W (MHPC_BWS_WT)
+__device__ __forceinline__ constexpr int widx(int r, int col) {
+  return MHPC_BWS_WT ? col * WR + r : r * WS + col;
+}
+__device__ __forceinline__ constexpr int g2idx(int r, int col) {
+  return MHPC_BWS_WT ? col * 2 + r : r * WS + col;
+}
+template <int NX> constexpr int JtStride = MHPC_BWS_WT ? (NX == 14 ? 18 : 10) : NX + MHPC_BWS_JTPAD;
+constexpr int JtOff = MHPC_BWS_WT ? 1 : 0;
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
   static constexpr int QS = NX == 14 ? 22 : 13;  // row stride of Q; column QV holds Qv
@@ -44,14 +62,14 @@ template <int NX> struct QShape {
 struct BwsLds {
   alignas(16) real H[196];
   alignas(16) real G[14];  // value function of knot k+1, then of knot k (row stride NX)
-  real W[7 * WS];      // rows NQ..NX-1 of [A B]
-  real G2[2 * WS];     // stance rows of [C D]
+  alignas(16) real W[MHPC_BWS_WT ? WS * WR : 7 * WS];  // rows NQ..NX-1 of [A B] (widx)
+  alignas(16) real G2[2 * WS];                         // stance rows of [C D] (g2idx)
   real l[JR];          // (lx, lu)
   real ldiag[18];      // diagonal running-cost Hessian (lxx, luu)
   real lyy2[4], ly2[2];
   union {
     struct {
-      real Jt[JR * 15];  // [A B]' H   (NR x NX, row stride JtStride<NX>)
+      alignas(16) real Jt[JR * (MHPC_BWS_WT ? 18 : 15)];  // [A B]' H (NR x NX, JtStride<NX>)
       real Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
     };
     struct {
@@ -303,9 +321,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         const real hb = col0[isg ? bi : bi * NX];
         real sacc = a != real(0.0) ? a * hb : real(0.0);
 #pragma unroll
-        for (int r = 0; r < NQ; ++r) sacc += sh.W[r * WS + row] * hc[r];
+        for (int r = 0; r < NQ; ++r) sacc += sh.W[widx(r, row)] * hc[r];
         real tt = real(0.0);
-        if (HAS_Y) tt = sh.G2[row] * ly0 + sh.G2[WS + row] * ly1;
+        if (HAS_Y) tt = sh.G2[g2idx(0, row)] * ly0 + sh.G2[g2idx(1, row)] * ly1;
         const real gs = (sh.l[row] + sacc) + tt;
         acc[u] = isg ? gs : sacc;
       }
@@ -313,7 +331,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int u = 0; u < C; ++u) {
         if (t0 + u >= T2) continue;
         const int row = g + GR * (t0 + u);
-        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * JtStride<NX> + j];
+        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * JtStride<NX> + JtOff + j];
         *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
       }
     }
@@ -332,10 +350,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const bool wr = g < RG;
     real jr[NQ];
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * JtStride<NX> + NQ + r];
+    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * JtStride<NX> + JtOff + NQ + r];
     real c0 = real(0.0), c1 = real(0.0);
     if (HAS_Y) {
-      const real gr0 = sh.G2[row], gr1 = sh.G2[WS + row];
+      const real gr0 = sh.G2[g2idx(0, row)], gr1 = sh.G2[g2idx(1, row)];
       c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
       c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
     }
@@ -349,13 +367,13 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
         const real a = coef_a<NQ>(col, dt);
-        const real jb = sh.Jt[row * JtStride<NX> + coef_b<NQ>(col)];
+        const real jb = sh.Jt[row * JtStride<NX> + JtOff + coef_b<NQ>(col)];
         real sacc = a != real(0.0) ? a * jb : real(0.0);
 #pragma unroll
-        for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[r * WS + col];
+        for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[widx(r, col)];
         const real base = row == col ? dg : real(0.0);
         real e2 = real(0.0);
-        if (HAS_Y) e2 = c0 * sh.G2[col] + c1 * sh.G2[WS + col];
+        if (HAS_Y) e2 = c0 * sh.G2[g2idx(0, col)] + c1 * sh.G2[g2idx(1, col)];
         real v = (base + e2) + sacc;
         const real vr = v + real(1.0) * reg;
         acc[u] = row == col ? vr : v;
@@ -779,11 +797,11 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     if (e < PS_JAC) {
       const int col = e / 9, r = e - col * 9;
       if (r < 7) {
-        dst[t] = (int)(sh.W - shf) + r * WS + col;
+        dst[t] = (int)(sh.W - shf) + widx(r, col);
         mul[t] = dt;
         base[t] = col == 7 + r ? real(1.0) : real(0.0);
       } else if (stance) {
-        dst[t] = (int)(sh.G2 - shf) + (r - 7) * WS + col;
+        dst[t] = (int)(sh.G2 - shf) + g2idx(r - 7, col);
       }
     } else if (e < PS) {
       const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
@@ -879,13 +897,13 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     if (full) {
       if (lane < 30) {
         const int r = lane / 10, col = lane - r * 10;
-        sh.W[r * WS + col] = srb_w_entry(r, col, xs, us, foot, cs, dt);
+        sh.W[widx(r, col)] = srb_w_entry(r, col, xs, us, foot, cs, dt);
       }
     } else {
-      sh.W[2 * WS + 0] = srb_w_entry(2, 0, xs, us, foot, cs, dt);
-      sh.W[2 * WS + 1] = srb_w_entry(2, 1, xs, us, foot, cs, dt);
+      sh.W[widx(2, 0)] = srb_w_entry(2, 0, xs, us, foot, cs, dt);
+      sh.W[widx(2, 1)] = srb_w_entry(2, 1, xs, us, foot, cs, dt);
 #pragma unroll
-      for (int c = 6; c < 10; ++c) sh.W[2 * WS + c] = srb_w_entry(2, c, xs, us, foot, cs, dt);
+      for (int c = 6; c < 10; ++c) sh.W[widx(2, c)] = srb_w_entry(2, c, xs, us, foot, cs, dt);
     }
     const real rxi = lane == 30 ? pk : fb_rx;
     shf[dl] = fb_w2 * (own - rxi);
@@ -1081,6 +1099,10 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
 // part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).  The SRB half reads no
 // partials record and needs few registers (the WB code is not instantiated), so a partials
 // wave fits beside it on a SIMD.
+// Waves per SIMD the register allocator targets in the beyond-one-wave-per-SIMD build.
+#ifndef MHPC_BWS_MW
+#define MHPC_BWS_MW 2
+#endif
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, int part,
                       hipStream_t s) {
 #ifdef MHPC_BWS_WAVES
@@ -1099,11 +1121,11 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
   else if (v == MHPC_VARIANT_BWS_1WAVE && part == 2)
     hipLaunchKernelGGL((k_bws<64, 1, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_2WAVE && part == 2)
-    hipLaunchKernelGGL((k_bws<64, 2, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<64, MHPC_BWS_MW, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_1WAVE)
     hipLaunchKernelGGL((k_bws<64, 1, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else if (v == MHPC_VARIANT_BWS_2WAVE)
-    hipLaunchKernelGGL((k_bws<64, 2, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
+    hipLaunchKernelGGL((k_bws<64, MHPC_BWS_MW, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
   else
     hipLaunchKernelGGL((k_bws<128, 1, 0>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
 #endif
