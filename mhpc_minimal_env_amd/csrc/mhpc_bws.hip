@@ -53,6 +53,12 @@ __device__ __forceinline__ constexpr int g2idx(int r, int col) {
 }
 template <int NX> constexpr int JtStride = MHPC_BWS_WT ? (NX == 14 ? 18 : 10) : NX + MHPC_BWS_JTPAD;
 constexpr int JtOff = MHPC_BWS_WT ? 1 : 0;
+// The NU = 4 control rows of Q ([Qux | Quu | Qu]) column-major in U (MHPC_BWS_UT=1, default):
+// R45 / R5 read a column of them (Qux[.][j], Qu) as two ds_read_b128 instead of four strided
+// reads.  uidx(c, k) = row NX + k, column c.
+#ifndef MHPC_BWS_UT
+#define MHPC_BWS_UT 1
+#endif
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
   static constexpr int QS = NX == 14 ? 22 : 13;  // row stride of Q; column QV holds Qv
@@ -71,6 +77,7 @@ struct BwsLds {
     struct {
       alignas(16) real Jt[JR * (MHPC_BWS_WT ? 18 : 15)];  // [A B]' H (NR x NX, JtStride<NX>)
       real Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
+      alignas(16) real U[22 * 4];  // rows NX..NX+3 of Q column-major (MHPC_BWS_UT)
     };
     struct {
       real H2[196];      // impact-aware step: lifted H' and (Px' H2)
@@ -91,6 +98,11 @@ struct BwsLds {
   unsigned long long cyc[12], tlast;
 #endif
 };
+
+// Q entry (row NX + k, column c): in U (MHPC_BWS_UT) or in Q (row stride qs)
+__device__ __forceinline__ real& qu(BwsLds& sh, int qs, int nx, int k, int c) {
+  return MHPC_BWS_UT ? sh.U[c * 4 + k] : sh.Q[(nx + k) * qs + c];
+}
 
 // Optional cycle accounting per Riccati round (build with -DMHPC_BWS_TIMING; read with
 // mhpc_dbg_bws_cycles): slot i accumulates the cycles since the previous mark.
@@ -269,7 +281,7 @@ __device__ __forceinline__ int coef_b(int col) {
 // One Riccati knot.  On entry sh.{W,G2,l,lxx,luu,lyy2,ly2} hold the knot's derivatives and
 // sh.{H,G} the value function of knot k+1; on exit sh.{H,G} hold that of knot k.
 #ifndef MHPC_BWS_CH2
-#define MHPC_BWS_CH2 3
+#define MHPC_BWS_CH2 5
 #endif
 #ifndef MHPC_BWS_CH3
 #define MHPC_BWS_CH3 2
@@ -331,7 +343,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int u = 0; u < C; ++u) {
         if (t0 + u >= T2) continue;
         const int row = g + GR * (t0 + u);
-        real* dst = isg ? &sh.Q[row * QS + QV] : &sh.Jt[row * JtStride<NX> + JtOff + j];
+        real* dqv = &sh.Q[row * QS + QV];
+        if (MHPC_BWS_UT)  // Qu rows to U; padding rows (>= NR) to the junk slot
+          dqv = row < NX ? dqv : row < NR ? &sh.U[QV * 4 + (row - NX)] : &sh.junk[lane & 63];
+        real* dst = isg ? dqv : &sh.Jt[row * JtStride<NX> + JtOff + j];
         *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
       }
     }
@@ -382,7 +397,8 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int u = 0; u < C; ++u) {
         if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
-        *(wr ? &sh.Q[row * QS + col] : &sh.junk[lane & 63]) = acc[u];
+        real* dq = MHPC_BWS_UT && row >= NX ? &sh.U[col * 4 + (row - NX)] : &sh.Q[row * QS + col];
+        *(wr ? dq : &sh.junk[lane & 63]) = acc[u];
       }
     }
   }
@@ -394,7 +410,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
   // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
   real q0[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) q0[c] = sh.Q[NX * QS + NX + c];
+  for (int c = 0; c < 4; ++c) q0[c] = qu(sh, QS, NX, 0, NX + c);
   real adj = real(0.0);
   bool psd;
   {
@@ -403,8 +419,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const int i = (lane >> 2) & 3, j = lane & 3;  // lanes 0..15 of every wave
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
-    const real* q = &sh.Q[NX * QS + NX];
-#define QM(r, c) q[(r) * QS + (c)]
+#define QM(r, c) qu(sh, QS, NX, r, NX + (c))
     const real m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
     const real m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
     const real m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
@@ -414,7 +429,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        A[a * 4 + c] = sh.Q[(NX + a) * QS + NX + c] - (a == c ? real(1.0) * eps9 : real(0.0));
+        A[a * 4 + c] = qu(sh, QS, NX, a, NX + c) - (a == c ? real(1.0) * eps9 : real(0.0));
 #if MHPC_BWS_PSD == 1
     psd = ldlt_nopiv_is_positive4(A);
 #elif MHPC_BWS_PSD == 2
@@ -471,8 +486,8 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     for (int c = 0; c < 4; ++c) {
       real t = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t += sh.Q[(NX + k) * QS + QV] * inv[k * 4 + c];
-      s += t * sh.Q[(NX + c) * QS + QV];
+      for (int k = 0; k < 4; ++k) t += qu(sh, QS, NX, k, QV) * inv[k * 4 + c];
+      s += t * qu(sh, QS, NX, c, QV);
     }
     // s and psd are uniform: every lane of wave 0 writes the same value (no divergent
     // branch); the other waves of a 128-thread block must not re-read the updated dV
@@ -488,7 +503,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const int si = i < NX ? i : QV;
     real qi[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) qi[k] = sh.Q[(NX + k) * QS + si];
+    for (int k = 0; k < 4; ++k) qi[k] = qu(sh, QS, NX, k, si);
     real tq[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -511,7 +526,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         const int sj = j < NX ? j : QV;
         real sacc = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) sacc += tq[c] * sh.Q[(NX + c) * QS + sj];
+        for (int c = 0; c < 4; ++c) sacc += tq[c] * qu(sh, QS, NX, c, sj);
         const real qij = sh.Q[i * QS + sj];
         const real qji = sh.Q[(j < NX ? j : 0) * QS + i];
         const real sym = (qij + qji) / 2;
