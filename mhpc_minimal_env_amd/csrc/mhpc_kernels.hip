@@ -47,6 +47,17 @@ using real2 = float2;
 using real2 = double2;
 #endif
 
+// Feedback term K[i] (x - x_nom) of the line-search control (SinglePhase.cpp forward sweep,
+// u = u_nom + eps du + K dx), summed in column order.  (Summing the two halves of the row
+// separately -- a chain half as long -- measured no faster: profiles/r02_ab_wt_layout.txt.)
+template <int N>
+__device__ __forceinline__ real fb_dot(const real* Kr, const real* x, const real* nk) {
+  real fb = 0;
+#pragma unroll
+  for (int c = 0; c < N; ++c) fb += Kr[c] * (x[c] - nk[c]);
+  return fb;
+}
+
 // native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
 typedef real sreal2 __attribute__((ext_vector_type(2)));
 constexpr int ST_PPW = 6;      // problems per staged wave (64 lanes / 10 candidates)
@@ -290,9 +301,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           const int r0 = back ? 2 : 0;
 #pragma unroll
           for (int ii = 0; ii < 2; ++ii) {
-            real fb = 0;
-#pragma unroll
-            for (int c = 0; c < 14; ++c) fb += Kk[(r0 + ii) * 14 + c] * (x[c] - nk[c]);
+            const real fb = fb_dot<14>(Kk + (r0 + ii) * 14, x, nk);
             u2[ii] = (nk[14 + r0 + ii] + eps * duk[r0 + ii]) + fb;
           }
 #ifdef MHPC_RO_TIMING
@@ -315,9 +324,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           real u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            real fb = 0;
-#pragma unroll
-            for (int c = 0; c < 14; ++c) fb += Kk[i * 14 + c] * (x[c] - nk[c]);
+            const real fb = fb_dot<14>(Kk + i * 14, x, nk);
             u[i] = (nk[14 + i] + eps * duk[i]) + fb;
           }
 #ifdef MHPC_RO_TIMING
@@ -338,9 +345,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           real u[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            real fb = 0;
-#pragma unroll
-            for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
+            const real fb = fb_dot<6>(Kk + i * 6, x, nk);
             u[i] = (nk[6 + i] + eps * duk[i]) + fb;
           }
 #ifdef MHPC_RO_TIMING
@@ -571,9 +576,7 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
         real u[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          real fb = 0;
-#pragma unroll
-          for (int c = 0; c < 14; ++c) fb += Kk[i * 14 + c] * (x[c] - nk[c]);
+          const real fb = fb_dot<14>(Kk + i * 14, x, nk);
           u[i] = (nk[14 + i] + eps * duk[i]) + fb;
         }
         real xd[14], y[4];
@@ -618,9 +621,7 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
         real u[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          real fb = 0;
-#pragma unroll
-          for (int c = 0; c < 6; ++c) fb += Kk[i * 6 + c] * (x[c] - nk[c]);
+          const real fb = fb_dot<6>(Kk + i * 6, x, nk);
           u[i] = (nk[6 + i] + eps * duk[i]) + fb;
         }
         real xd[6];
@@ -825,8 +826,12 @@ __device__ __forceinline__ void partials_knot(const real* nk, real* rec) {
   }
 }
 
+// MHPC_PAR_MINB: blocks per CU the register allocator must allow for the partials (1: no cap)
+#ifndef MHPC_PAR_MINB
+#define MHPC_PAR_MINB 1
+#endif
 template <int G>
-__global__ __launch_bounds__(256) void k_partials(SolveParams sp, DevBufs d) {
+__global__ __launch_bounds__(256, MHPC_PAR_MINB) void k_partials(SolveParams sp, DevBufs d) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int b = (int)(t / sp.par_knots);
   if (b >= sp.B) return;
