@@ -52,6 +52,7 @@ using real2 = double2;
 // separately -- a chain half as long -- measured no faster: profiles/r02_ab_wt_layout.txt.)
 template <int N>
 __device__ __forceinline__ real fb_dot(const real* Kr, const real* x, const real* nk) {
+  MHPC_NO_FMA_F32  // as in the kernels that call it (fp32 line search uncontracted)
   real fb = 0;
 #pragma unroll
   for (int c = 0; c < N; ++c) fb += Kr[c] * (x[c] - nk[c]);

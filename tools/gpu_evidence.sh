@@ -25,4 +25,4 @@ import json
 for l in open('gpurun_out/sweep_${TAG}.jsonl'):
     d = json.loads(l); print('sweep', d['batch'], round(d['value']), 'solves/s', round(d['ms_per_step'], 3), 'ms')
 "
-bash tools/gpu_profile.sh ${TAG}_b1024 1024 && bash tools/gpu_profile.sh ${TAG}_b4096 4096 && B=1024 bash tools/gpu_pmc_stalls.sh ${TAG}_sq > gpurun_out/sq_${TAG}.txt 2>&1
+bash tools/gpu_profile.sh ${TAG}_b1024 1024 && bash tools/gpu_profile.sh ${TAG}_b4096 4096 && WL=c5 bash tools/gpu_profile.sh ${TAG}_c5_b4096 4096 && B=1024 bash tools/gpu_pmc_stalls.sh ${TAG}_sq > gpurun_out/sq_${TAG}.txt 2>&1
