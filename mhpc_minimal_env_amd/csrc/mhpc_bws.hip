@@ -59,9 +59,17 @@ constexpr int JtOff = MHPC_BWS_WT ? 1 : 0;
 #ifndef MHPC_BWS_UT
 #define MHPC_BWS_UT 1
 #endif
+// Row stride of Q for the WB knot and column stride of U (bank spreading of R3's writes and
+// R5's reads: tools/lds_bank_model.py)
+#ifndef MHPC_BWS_QS14
+#define MHPC_BWS_QS14 22
+#endif
+#ifndef MHPC_BWS_US
+#define MHPC_BWS_US 4
+#endif
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
-  static constexpr int QS = NX == 14 ? 22 : 13;  // row stride of Q; column QV holds Qv
+  static constexpr int QS = NX == 14 ? MHPC_BWS_QS14 : 13;  // row stride of Q; column QV holds Qv
   static constexpr int QV = QS - 1;
 };
 
@@ -76,8 +84,8 @@ struct BwsLds {
   union {
     struct {
       alignas(16) real Jt[JR * (MHPC_BWS_WT ? 18 : 15)];  // [A B]' H (NR x NX, JtStride<NX>)
-      real Q[QR * 22];   // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
-      alignas(16) real U[22 * 4];  // rows NX..NX+3 of Q column-major (MHPC_BWS_UT)
+      real Q[QR * MHPC_BWS_QS14];  // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
+      alignas(16) real U[MHPC_BWS_QS14 * MHPC_BWS_US];  // rows NX..NX+3 of Q column-major (MHPC_BWS_UT)
     };
     struct {
       real H2[196];      // impact-aware step: lifted H' and (Px' H2)
@@ -101,7 +109,7 @@ struct BwsLds {
 
 // Q entry (row NX + k, column c): in U (MHPC_BWS_UT) or in Q (row stride qs)
 __device__ __forceinline__ real& qu(BwsLds& sh, int qs, int nx, int k, int c) {
-  return MHPC_BWS_UT ? sh.U[c * 4 + k] : sh.Q[(nx + k) * qs + c];
+  return MHPC_BWS_UT ? sh.U[c * MHPC_BWS_US + k] : sh.Q[(nx + k) * qs + c];
 }
 
 // Optional cycle accounting per Riccati round (build with -DMHPC_BWS_TIMING; read with
@@ -345,7 +353,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         const int row = g + GR * (t0 + u);
         real* dqv = &sh.Q[row * QS + QV];
         if (MHPC_BWS_UT)  // Qu rows to U; padding rows (>= NR) to the junk slot
-          dqv = row < NX ? dqv : row < NR ? &sh.U[QV * 4 + (row - NX)] : &sh.junk[lane & 63];
+          dqv = row < NX ? dqv : row < NR ? &sh.U[QV * MHPC_BWS_US + (row - NX)] : &sh.junk[lane & 63];
         real* dst = isg ? dqv : &sh.Jt[row * JtStride<NX> + JtOff + j];
         *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
       }
@@ -397,7 +405,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
       for (int u = 0; u < C; ++u) {
         if (t0 + u >= T3) continue;
         const int col = g + RG * (t0 + u);
-        real* dq = MHPC_BWS_UT && row >= NX ? &sh.U[col * 4 + (row - NX)] : &sh.Q[row * QS + col];
+        real* dq = MHPC_BWS_UT && row >= NX ? &sh.U[col * MHPC_BWS_US + (row - NX)] : &sh.Q[row * QS + col];
         *(wr ? dq : &sh.junk[lane & 63]) = acc[u];
       }
     }
