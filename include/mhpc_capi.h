@@ -125,6 +125,11 @@ int mhpc_solve(mhpc_handle* h, int32_t* status);
  * K [batch][N][4][xsize], Vx [batch][N][xsize]. */
 int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, double* K,
                    double* du, double* Vx);
+/* mhpc_get_phase for problems [first, first + count) of the batch only (shapes with
+ * count in place of batch): one problem's phase, as the reference's single-problem
+ * _phases[p]->get_nominal_ms_ptr() / get_CTG_info_ptr() hold it (SinglePhaseAbstract.h:79-81). */
+int mhpc_get_phase_problems(mhpc_handle* h, int phase, int first, int count, double* x, double* u,
+                            double* y, double* K, double* du, double* Vx);
 /* J, dV_exp, viol: [batch]; V_phase, dV_phase: [batch][n_phases]; trace: [batch][MHPC_TRACE_LEN]
  * (decision trace, encoding in DESIGN.md §Parity); any pointer may be NULL. */
 int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
@@ -149,6 +154,47 @@ typedef struct {
 int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait);
 /* The handle's current phase layout (changes with mhpc_update_problem). */
 int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc);
+
+/* ---- cost and constraint parameters (the reference's downward plugin points) --------
+ * The reference's solve reads its weights through CostAbstract / Cost<T,X,U,Y>
+ * (HSDDPSolver/header/CostBase.h:9-46: diagonal _Q, _R, _S, _Qf per mode) and its
+ * inequality / AL parameters through Constraint (ConstraintsBase.h:11-50: AL_REB_PARAMETER per
+ * mode), with the values MHPCCost.cpp:24-75 and MHPCConstraints.cpp:14-88 set.  A handle
+ * starts from those values; mhpc_set_* replaces them for every later solve (they travel in
+ * the kernels' parameter block).  Rows are modes 1..4. */
+typedef struct {
+  double wb_Q[4][14];  /* WBCost _Q diagonal (0.01 * q) */
+  double wb_R[4][4];   /* WBCost _R diagonal (0.5 * r[m]) */
+  double wb_S[4][4];   /* WBCost _S diagonal (s[m]; s[3] uninitialised in the reference: 0) */
+  double wb_Qf[4][14]; /* WBCost _Qf diagonal (100 * qf[m]) */
+  double fb_Q[4][6];   /* FBCost _Q diagonal (0.01 * q) */
+  double fb_R[4][4];   /* FBCost _R diagonal (r[m]); FBCost _S is zero (SRB y == 0) */
+  double fb_Qf[4][6];  /* FBCost _Qf diagonal (100 * qf) */
+} mhpc_cost_weights;
+
+typedef struct {
+  double torque_limit;     /* WBConstraint b_torque: -limit <= u_i <= limit (33) */
+  double friction_coeff;   /* WBConstraint _friccoeff of the GRF cone (0.5) */
+  double sigma[4];         /* AL penalty at initialisation, modes with a touchdown
+                              constraint (2, 4) only: 5 */
+  double delta[4];         /* ReB relaxation at initialisation (0.1) */
+  double delta_min[4];     /* its lower bound in the AL update (0.01) */
+  double eps_torque[4];    /* ReB weight of the torque limits (0.01) */
+  double eps_grf[4];       /* ReB weight of the GRF constraints, stance modes 1 / 3 (0.01) */
+  /* The joint limits carry eps_ReB = 0 in the reference (MHPCConstraints.cpp:60-82) and
+   * contribute exact zeros; they are not a parameter here. */
+} mhpc_constraint_params;
+
+/* The reference's values (MHPCCost.cpp:24-75, MHPCConstraints.cpp:14-88). */
+int mhpc_default_cost_weights(mhpc_cost_weights* w);
+int mhpc_default_constraint_params(mhpc_constraint_params* c);
+/* Replace / read the handle's parameters; take effect from the next mhpc_initialize /
+ * mhpc_update_problem (AL / ReB initial values) and mhpc_solve (weights, limits).  Every
+ * entry must be finite, weights >= 0, torque_limit > 0, delta and delta_min > 0. */
+int mhpc_set_cost_weights(mhpc_handle* h, const mhpc_cost_weights* w);
+int mhpc_get_cost_weights(mhpc_handle* h, mhpc_cost_weights* w);
+int mhpc_set_constraint_params(mhpc_handle* h, const mhpc_constraint_params* c);
+int mhpc_get_constraint_params(mhpc_handle* h, mhpc_constraint_params* c);
 
 /* Running-cost gradient lx of knots 0..N-2 ([batch][N-1][n]) and terminal-cost gradient Phix
  * ([batch][n]) of `phase` as the last partials evaluation left them: the reference's
@@ -210,10 +256,6 @@ void mhpc_destroy(mhpc_handle* h);
                                          so that one block's line search shares the chip with
                                          another block's sweep); 0 = automatic */
 #define MHPC_MAX_SUBBATCH 4
-#define MHPC_VARIANT_GRAPH 4          /* which: the solve's launch schedule as a HIP graph */
-#define MHPC_VARIANT_GRAPH_ON 1       /*   captured once per schedule, replayed */
-#define MHPC_VARIANT_GRAPH_OFF 2      /*   every launch issued from the host (default: the
-                                         replay measured no faster) */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

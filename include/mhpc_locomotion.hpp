@@ -7,14 +7,22 @@
 //   MHPCUserParameters     MHPC_CompoundTypes.h:242-251  (alias MHPC_UserParameter)
 //   GaitType2D, Gait       Gait.h:6-77
 //   MHPCLocomotion<T>      MHPCLocomotion.h:13-83 (initialization, solve_mhpc, print_debugInfo)
+//   MultiPhaseDDP<T>       MultiPhaseDDP.h:12-63 (public _phases, _n_phases, _option,
+//                          _actual_cost, _exp_cost_change, _tconstr_violation)
+//   SinglePhaseAbstract<T> SinglePhaseAbstract.h:66-134 (public _modeidx, _phaseidx, _dt,
+//                          _N_TIMESTEPS, _V, _dV, _xsize/_usize/_ysize, get_modeidx,
+//                          get_nominal_ms_ptr, get_CTG_info_ptr, get_terminal_state)
+//   ModelState, CostToGoStruct  MHPC_CompoundTypes.h:7-22,88-114 (x/u/y; G, du, K)
 // The heavy lifting happens in libmhpc_amd.so (HIP, gfx950).  Extensions: a batch of
 // independent problems per object, and set_initial_conditions() for per-problem x0.
 // Header-only; link with -lmhpc_amd.  Errors throw std::runtime_error on this side of
 // the ABI (none cross it).
 #pragma once
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <fstream>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -91,6 +99,117 @@ class Gait {
   std::vector<float> timing_;
 };
 
+// Fixed-size vector / matrix with Eigen's element access (v(i), v[i], m(r, c); m stored
+// column-major like Eigen's default), enough for reading solver output the way the
+// reference's callers read VecM / MatMN (MHPC_CPPTypes.h).
+template <typename T, size_t n>
+struct VecM {
+  T v[n] = {};
+  T& operator()(size_t i) { return v[i]; }
+  const T& operator()(size_t i) const { return v[i]; }
+  T& operator[](size_t i) { return v[i]; }
+  const T& operator[](size_t i) const { return v[i]; }
+  static constexpr size_t size() { return n; }
+  T* data() { return v; }
+  const T* data() const { return v; }
+};
+template <typename T, size_t r, size_t c>
+struct MatMN {
+  T v[r * c] = {};
+  T& operator()(size_t i, size_t j) { return v[j * r + i]; }
+  const T& operator()(size_t i, size_t j) const { return v[j * r + i]; }
+  static constexpr size_t rows() { return r; }
+  static constexpr size_t cols() { return c; }
+  T* data() { return v; }
+  const T* data() const { return v; }
+};
+
+// One knot of a phase's nominal trajectory (MHPC_CompoundTypes.h:7-22)
+template <typename T, size_t xsize, size_t usize, size_t ysize>
+struct ModelState {
+  VecM<T, xsize> x;
+  VecM<T, usize> u;
+  VecM<T, ysize> y;
+};
+
+// One knot of a phase's cost-to-go information (MHPC_CompoundTypes.h:88-101): the value
+// gradient G (Vx) and the feedback du, K that the execution horizon consumes.  The Hessian H
+// and the Q-function blocks are intermediates of the backward sweep that the device keeps
+// in LDS and never writes to HBM; they are not part of this struct (reading them fails to
+// compile instead of returning zeros).
+template <typename T, size_t xsize, size_t usize>
+struct CostToGoStruct {
+  VecM<T, xsize> G;
+  VecM<T, usize> du;
+  MatMN<T, usize, xsize> K;
+};
+
+// Read-only view of one phase of one problem of the batch after a solve, with the public
+// members and accessors of the reference's SinglePhaseAbstract (SinglePhaseAbstract.h:66-134).
+// The nominal / cost-to-go arrays are copied from the device on first access after a solve.
+template <typename T>
+class SinglePhaseAbstract {
+ public:
+  int _modeidx = 1;
+  int _phaseidx = 1;
+  T _dt = 0;
+  size_t _N_TIMESTEPS = 0;
+  T _V = 0;   // actual cost of this phase only
+  T _dV = 0;  // expected cost change of this phase
+  size_t _xsize = 0, _usize = 4, _ysize = 4;
+
+  size_t get_modeidx() const { return _modeidx; }
+  // ModelState<T, _xsize, 4, 4>[_N_TIMESTEPS] (cast as the reference's solve_mhpc does)
+  void* get_nominal_ms_ptr() { fetch(); return ms_.data(); }
+  // CostToGoStruct<T, _xsize, 4>[_N_TIMESTEPS]
+  void* get_CTG_info_ptr() { fetch(); return ctg_.data(); }
+  std::vector<T> get_terminal_state() {
+    fetch();
+    const T* xN = ms_.data() + (_N_TIMESTEPS - 1) * ms_stride();
+    return std::vector<T>(xN, xN + _xsize);
+  }
+
+ private:
+  template <typename>
+  friend class MHPCLocomotion;
+  size_t ms_stride() const {
+    return _xsize == 14 ? sizeof(ModelState<T, 14, 4, 4>) / sizeof(T)
+                        : sizeof(ModelState<T, 6, 4, 4>) / sizeof(T);
+  }
+  size_t ctg_stride() const {
+    return _xsize == 14 ? sizeof(CostToGoStruct<T, 14, 4>) / sizeof(T)
+                        : sizeof(CostToGoStruct<T, 6, 4>) / sizeof(T);
+  }
+  void fetch() {
+    if (!stale_) return;
+    const size_t n = _xsize, N = _N_TIMESTEPS;
+    std::vector<double> x(N * n), u(N * 4), y(N * 4), K(N * 4 * n), du(N * 4), G(N * n);
+    const int rc = mhpc_get_phase_problems(h_, phase_, problem_, 1, x.data(), u.data(), y.data(),
+                                           K.data(), du.data(), G.data());
+    if (rc != MHPC_OK)
+      throw std::runtime_error(std::string("mhpc_get_phase_problems: ") + mhpc_last_error());
+    const size_t ms = ms_stride(), cs = ctg_stride();
+    ms_.assign(N * ms, T(0));
+    ctg_.assign(N * cs, T(0));
+    for (size_t k = 0; k < N; ++k) {
+      T* m = &ms_[k * ms];  // x, u, y contiguous (ModelState's member order)
+      for (size_t i = 0; i < n; ++i) m[i] = (T)x[k * n + i];
+      for (size_t i = 0; i < 4; ++i) m[n + i] = (T)u[k * 4 + i];
+      for (size_t i = 0; i < 4; ++i) m[n + 4 + i] = (T)y[k * 4 + i];
+      T* c = &ctg_[k * cs];  // G, du, K (column-major 4 x n)
+      for (size_t i = 0; i < n; ++i) c[i] = (T)G[k * n + i];
+      for (size_t i = 0; i < 4; ++i) c[n + i] = (T)du[k * 4 + i];
+      for (size_t r = 0; r < 4; ++r)
+        for (size_t j = 0; j < n; ++j) c[n + 4 + j * 4 + r] = (T)K[(k * 4 + r) * n + j];
+    }
+    stale_ = false;
+  }
+  mhpc_handle* h_ = nullptr;
+  int phase_ = 0, problem_ = 0;
+  bool stale_ = true;
+  std::vector<T> ms_, ctg_;
+};
+
 template <typename TH>
 class MHPCLocomotion {
  public:
@@ -121,6 +240,11 @@ class MHPCLocomotion {
                              option.DDP_thresh, option.AL_thresh, option.AL_active,
                              option.ReB_active, option.smooth_active, 0};
     check(mhpc_create(&desc_, &opt_, batch_, device, &h_), "mhpc_create");
+    _option = option;
+    _n_phases = np;
+    for (int p = 0; p < np; ++p) phase_store_.emplace_back(new SinglePhaseAbstract<TH>());
+    for (auto& q : phase_store_) _phases.push_back(q.get());
+    refresh_phases(false);
     gait_ = gait->to_c();
     // default initial condition (MHPCLocomotion.cpp:37-39), projected if phase 0 is SRB
     const double x0[14] = {0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098,
@@ -150,6 +274,7 @@ class MHPCLocomotion {
     check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
     check(mhpc_update_problem(h_, &gait_), "mhpc_update_problem");
     check(mhpc_get_desc(h_, &desc_), "mhpc_get_desc");
+    refresh_phases(false);
   }
 
   // execution horizon of solve_mhpc (ms_exec / CTG_exec, MHPCLocomotion.cpp:176-194): nominal
@@ -187,17 +312,21 @@ class MHPCLocomotion {
   void initialization() {  // (:47-53)
     check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
     check(mhpc_initialize(h_), "mhpc_initialize");
+    refresh_phases(false);
   }
 
   void solve_mhpc() {  // (:167-195)
     status_.assign(batch_, 0);
     check(mhpc_solve(h_, status_.data()), "mhpc_solve");
-    std::vector<double> J(batch_), dV(batch_), viol(batch_);
-    check(mhpc_get_scalars(h_, J.data(), dV.data(), viol.data(), nullptr, nullptr, nullptr),
-          "mhpc_get_scalars");
-    _actual_cost = J[0];
-    _exp_cost_change = dV[0];
-    _tconstr_violation = viol[0];
+    refresh_phases(true);
+  }
+
+  // extension: which problem of the batch _phases, _actual_cost, _exp_cost_change and
+  // _tconstr_violation describe (default 0; the reference holds exactly one problem)
+  void select_problem(int b) {
+    if (b < 0 || b >= batch_) throw std::runtime_error("select_problem: no such problem");
+    problem_ = b;
+    refresh_phases(solved_);
   }
 
   // MHPCLocomotion::print_debugInfo (MHPCLocomotion.cpp:293-380) for one problem:
@@ -257,13 +386,66 @@ class MHPCLocomotion {
     }
   }
 
+  // extension: the weights / constraint parameters the reference's WBCost, FBCost and
+  // WBConstraint objects hold (MHPCCost.cpp:24-75, MHPCConstraints.cpp:14-88), replaceable
+  // here for every later solve (mhpc_set_cost_weights / mhpc_set_constraint_params)
+  void set_cost_weights(const mhpc_cost_weights& w) {
+    check(mhpc_set_cost_weights(h_, &w), "mhpc_set_cost_weights");
+  }
+  mhpc_cost_weights get_cost_weights() {
+    mhpc_cost_weights w{};
+    check(mhpc_get_cost_weights(h_, &w), "mhpc_get_cost_weights");
+    return w;
+  }
+  void set_constraint_params(const mhpc_constraint_params& c) {
+    check(mhpc_set_constraint_params(h_, &c), "mhpc_set_constraint_params");
+  }
+  mhpc_constraint_params get_constraint_params() {
+    mhpc_constraint_params c{};
+    check(mhpc_get_constraint_params(h_, &c), "mhpc_get_constraint_params");
+    return c;
+  }
+
   const std::vector<int32_t>& status() const { return status_; }
   const mhpc_problem_desc& desc() const { return desc_; }
   mhpc_handle* handle() { return h_; }
 
   TH _actual_cost = 0, _exp_cost_change = 0, _tconstr_violation = 0;
+  // MultiPhaseDDP's public phase list: _phases[p]->_V, _dV, _N_TIMESTEPS, get_nominal_ms_ptr()...
+  std::vector<SinglePhaseAbstract<TH>*> _phases;
+  int _n_phases = 0;
+  HSDDP_OPTION<TH> _option;
 
  private:
+  // phase configuration from the handle's current layout; costs from the last solve
+  void refresh_phases(bool scalars) {
+    const int np = desc_.n_wb + desc_.n_fb;
+    std::vector<double> J(batch_), dV(batch_), viol(batch_), Vp((size_t)batch_ * np),
+        dVp((size_t)batch_ * np);
+    if (scalars)
+      check(mhpc_get_scalars(h_, J.data(), dV.data(), viol.data(), Vp.data(), dVp.data(), nullptr),
+            "mhpc_get_scalars");
+    solved_ = scalars;
+    for (int p = 0; p < np; ++p) {
+      SinglePhaseAbstract<TH>& q = *_phases[p];
+      q.h_ = h_;
+      q.phase_ = p;
+      q.problem_ = problem_;
+      q.stale_ = true;
+      q._modeidx = desc_.mode_seq[p];
+      q._phaseidx = p;
+      q._dt = p < desc_.n_wb ? desc_.dt_wb : desc_.dt_fb;
+      q._N_TIMESTEPS = desc_.N[p];
+      q._xsize = p < desc_.n_wb ? 14 : 6;
+      q._V = scalars ? (TH)Vp[(size_t)problem_ * np + p] : TH(0);
+      q._dV = scalars ? (TH)dVp[(size_t)problem_ * np + p] : TH(0);
+    }
+    if (scalars) {
+      _actual_cost = J[problem_];
+      _exp_cost_change = dV[problem_];
+      _tconstr_violation = viol[problem_];
+    }
+  }
   static void check(int rc, const char* what) {
     if (rc != MHPC_OK)
       throw std::runtime_error(std::string(what) + ": " + mhpc_last_error());
@@ -294,4 +476,7 @@ class MHPCLocomotion {
   mhpc_handle* h_ = nullptr;
   std::vector<double> x0_;
   std::vector<int32_t> status_;
+  std::vector<std::unique_ptr<SinglePhaseAbstract<TH>>> phase_store_;
+  int problem_ = 0;
+  bool solved_ = false;
 };

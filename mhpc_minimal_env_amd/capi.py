@@ -30,8 +30,6 @@ RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged"
 MHPC_VARIANT_OVERLAP = 2
 OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_VARIANT_SUBBATCH = 3
-MHPC_VARIANT_GRAPH = 4
-GRAPH_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_MAX_SUBBATCH = 4
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1
@@ -107,6 +105,56 @@ class HsddpOption(ctypes.Structure):
     ]
 
 
+def _mat(r, c):
+    return (ctypes.c_double * c) * r
+
+
+class CostWeights(ctypes.Structure):
+    """mhpc_cost_weights: diagonal weights per mode (CostBase.h:9-46, MHPCCost.cpp:24-75)."""
+    _fields_ = [
+        ("wb_Q", _mat(4, 14)), ("wb_R", _mat(4, 4)), ("wb_S", _mat(4, 4)), ("wb_Qf", _mat(4, 14)),
+        ("fb_Q", _mat(4, 6)), ("fb_R", _mat(4, 4)), ("fb_Qf", _mat(4, 6)),
+    ]
+
+    def as_dict(self) -> dict:
+        import numpy as np
+        return {k: np.ctypeslib.as_array(getattr(self, k)).copy() for k, _ in self._fields_}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "CostWeights":
+        import numpy as np
+        w = cls()
+        for k, _ in cls._fields_:
+            np.ctypeslib.as_array(getattr(w, k))[...] = np.asarray(d[k], dtype=np.float64)
+        return w
+
+
+class ConstraintParams(ctypes.Structure):
+    """mhpc_constraint_params (ConstraintsBase.h:11-50, MHPCConstraints.cpp:14-88)."""
+    _fields_ = [
+        ("torque_limit", ctypes.c_double), ("friction_coeff", ctypes.c_double),
+        ("sigma", ctypes.c_double * 4), ("delta", ctypes.c_double * 4),
+        ("delta_min", ctypes.c_double * 4), ("eps_torque", ctypes.c_double * 4),
+        ("eps_grf", ctypes.c_double * 4),
+    ]
+
+    def as_dict(self) -> dict:
+        import numpy as np
+        return {k: (float(getattr(self, k)) if t is ctypes.c_double
+                    else np.ctypeslib.as_array(getattr(self, k)).copy()) for k, t in self._fields_}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "ConstraintParams":
+        import numpy as np
+        c = cls()
+        for k, t in cls._fields_:
+            if t is ctypes.c_double:
+                setattr(c, k, float(d[k]))
+            else:
+                np.ctypeslib.as_array(getattr(c, k))[...] = np.asarray(d[k], dtype=np.float64)
+        return c
+
+
 class Counters(ctypes.Structure):
     _fields_ = [
         ("ddp_iters", ctypes.c_int64),
@@ -134,6 +182,8 @@ SIGNATURES = [
     ("mhpc_initialize", ctypes.c_int, [ctypes.c_void_p]),
     ("mhpc_solve", ctypes.c_int, [ctypes.c_void_p, _IP]),
     ("mhpc_get_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP]),
+    ("mhpc_get_phase_problems", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, _DP, _DP, _DP, _DP, _DP, _DP]),
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
     ("mhpc_get_cost_gradients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP]),
@@ -149,6 +199,12 @@ SIGNATURES = [
     ("mhpc_reset_kernel_stats", ctypes.c_int, [ctypes.c_void_p]),
     ("mhpc_get_kernel_flops", ctypes.c_int, [ctypes.c_void_p, _DP]),
     ("mhpc_set_kernel_variant", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    ("mhpc_default_cost_weights", ctypes.c_int, [ctypes.POINTER(CostWeights)]),
+    ("mhpc_default_constraint_params", ctypes.c_int, [ctypes.POINTER(ConstraintParams)]),
+    ("mhpc_set_cost_weights", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CostWeights)]),
+    ("mhpc_get_cost_weights", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CostWeights)]),
+    ("mhpc_set_constraint_params", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ConstraintParams)]),
+    ("mhpc_get_constraint_params", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ConstraintParams)]),
     ("mhpc_eval_wb_dynamics", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP, _DP,
                                              _DP, _DP]),
     ("mhpc_eval_wb_dynamics_pair", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _DP,
@@ -195,3 +251,15 @@ def dptr(a):
 
 def iptr(a):
     return None if a is None else a.ctypes.data_as(_IP)
+
+
+def default_cost_weights() -> CostWeights:
+    w = CostWeights()
+    check(lib().mhpc_default_cost_weights(ctypes.byref(w)), "mhpc_default_cost_weights")
+    return w
+
+
+def default_constraint_params() -> ConstraintParams:
+    c = ConstraintParams()
+    check(lib().mhpc_default_constraint_params(ctypes.byref(c)), "mhpc_default_constraint_params")
+    return c

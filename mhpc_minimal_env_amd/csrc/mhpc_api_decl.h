@@ -9,8 +9,9 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
 int api_set_x0(Handle* h, const double* x0);
 int api_initialize(Handle* h);
 int api_solve(Handle* h, int32_t* status);
-int api_get_phase(Handle* h, int phase, double* x, double* u, double* y, double* K, double* du,
-                  double* Vx);
+int api_get_phase(Handle* h, int phase, int first, int count, double* x, double* u, double* y,
+                  double* K, double* du, double* Vx);
+int api_batch(Handle* h);
 int api_get_scalars(Handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
                     double* dV_phase, int32_t* trace);
 int api_rollout_costs(Handle* h, int n_eps, const double* eps, double* J, double* viol, float* ms);
@@ -23,5 +24,9 @@ int api_get_kernel_stats(Handle* h, double* ms, int64_t* launches, double* alg_b
 int api_reset_kernel_stats(Handle* h);
 int api_get_kernel_flops(Handle* h, double* flops);
 int api_set_kernel_variant(Handle* h, int which, int variant);
+int api_set_cost_weights(Handle* h, const mhpc_cost_weights* w);
+int api_get_cost_weights(Handle* h, mhpc_cost_weights* w);
+int api_set_constraint_params(Handle* h, const mhpc_constraint_params* c);
+int api_get_constraint_params(Handle* h, mhpc_constraint_params* c);
 void api_destroy(Handle* h);
 }  // namespace API_NS

@@ -566,13 +566,14 @@ struct CostXConsts {
   real w2;   // 2 dt Q[i]
   real rx;   // reference of state i (unused for i = 0: the position reference)
 };
-__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, real dt) {
+__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, int mode,
+                                                        real dt) {
   CostXConsts c{real(0.0), real(0.0)};
   if (lane < 14) {
     const int i = lane;
     c.rx = i == 1 ? sp.height : i == 2 ? real(0.0) : (i >= 3 && i < 7) ? cQjointBias[i - 3]
            : i == 7 ? sp.vel : real(0.0);
-    c.w2 = 2 * dt * cQwb[i];
+    c.w2 = 2 * dt * sp.cw.wQ[mode - 1][i];
   }
   return c;
 }
@@ -636,7 +637,7 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
   for (int e = lane; e < NX * NX + NX; e += NT) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
-      real v = i == j ? (wb ? cQfwb[mode - 1][i] : cQffb[i]) : real(0.0);
+      real v = i == j ? (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) : real(0.0);
       if (al) {
         const int ai = i == 2 ? 0 : (i == ih ? 1 : (i == ih + 1 ? 2 : -1));
         const int aj = j == 2 ? 0 : (j == ih ? 1 : (j == ih + 1 ? 2 : -1));
@@ -649,7 +650,7 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
       real rxi;
       if (wb) rxi = i == 0 ? pos : (i == 7 ? sp.vel : cXtermWB[mode - 1][i]);
       else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : real(0.0)));
-      real v = (wb ? cQfwb[mode - 1][i] : cQffb[i]) * (xe[i] - rxi);
+      real v = (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) * (xe[i] - rxi);
       if (al) v += 50 * (s * s / 2 * sh.hx[i] * h + lam * sh.hx[i]);
       const real g = v + sh.G[i];
       sh.G[i] = g;
@@ -805,7 +806,7 @@ __device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, c
     const real* tk = traj_ptr(sp, d, b, nom, ko + k);
     prex = *(isref ? pos + k : tk + xo);
   };
-  const CostXConsts cx = wb_cost_x_consts(lane, sp, dt);
+  const CostXConsts cx = wb_cost_x_consts(lane, sp, sp.mode[p], dt);
   // Where each prefetched record element goes, fixed for the phase: value = pre * mul + base
   // into the LDS block at dst (W entries: (I + dt Ac | dt Bc), everything else verbatim:
   // x * 1 + (-0) == x exactly); elements with no target write the lane's junk slot.
@@ -884,11 +885,11 @@ __device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, c
   real fb_w2 = real(0.0), fb_rx = real(0.0);
   if (lane >= 30 && lane < 36) {
     const int i = lane - 30;
-    fb_w2 = 2 * dt * cQfb[i];
+    fb_w2 = 2 * dt * sp.cw.fQ[m][i];
     fb_rx = i == 1 ? sp.height : i == 3 ? sp.vel : real(0.0);
   } else if (lane >= 36 && lane < 40) {
     const int c = lane - 36;
-    fb_w2 = 2 * dt * cRfb[m][c];
+    fb_w2 = 2 * dt * sp.cw.fR[m][c];
     fb_rx = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
   }
   // every wave of the block loads the same nominal words (lane & 63), so the uniform W

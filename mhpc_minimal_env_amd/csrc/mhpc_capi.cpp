@@ -107,7 +107,14 @@ extern "C" int mhpc_initialize(mhpc_handle* h) { FWD(initialize); }
 extern "C" int mhpc_solve(mhpc_handle* h, int32_t* status) { FWD(solve, status); }
 extern "C" int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, double* K,
                               double* du, double* Vx) {
-  FWD(get_phase, phase, x, u, y, K, du, Vx);
+  int B = 0;
+  if (h) B = h->precision == 32 ? mhpc32::api_batch((mhpc32::Handle*)h->impl)
+                                : mhpc::api_batch((mhpc::Handle*)h->impl);
+  FWD(get_phase, phase, 0, B, x, u, y, K, du, Vx);
+}
+extern "C" int mhpc_get_phase_problems(mhpc_handle* h, int phase, int first, int count, double* x,
+                                       double* u, double* y, double* K, double* du, double* Vx) {
+  FWD(get_phase, phase, first, count, x, u, y, K, du, Vx);
 }
 extern "C" int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol,
                                 double* V_phase, double* dV_phase, int32_t* trace) {
@@ -134,6 +141,69 @@ extern "C" int mhpc_reset_kernel_stats(mhpc_handle* h) { FWD(reset_kernel_stats)
 extern "C" int mhpc_get_kernel_flops(mhpc_handle* h, double* flops) { FWD(get_kernel_flops, flops); }
 extern "C" int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant) {
   FWD(set_kernel_variant, which, variant);
+}
+// MHPCCost.cpp:24-75 (WBCost / FBCost::set_weighting_matrices): diagonals per mode.
+extern "C" int mhpc_default_cost_weights(mhpc_cost_weights* w) {
+  if (!w) {
+    mhpc_g_err = "null argument";
+    return MHPC_ERR_INVALID;
+  }
+  static const double q[14] = {0, 10, 5, 4, 4, 4, 4, 2, 1, .01, 6, 6, 6, 6};
+  static const double qf[4][14] = {{0, 20, 8, 3, 3, 3, 3, 3, 2, 0.01, 5, 5, 0.01, 0.01},
+                                   {0, 20, 8, 3, 3, 3, 3, 3, 2, 0.01, 5, 5, 5, 5},
+                                   {0, 20, 8, 3, 3, 3, 3, 3, 2, 0.01, 0.01, 0.01, 5, 5},
+                                   {0, 20, 8, 3, 3, 3, 3, 3, 2, 0.01, 5, 5, 5, 5}};
+  static const double r[4][4] = {{5, 5, 1, 1}, {1, 1, 1, 1}, {1, 1, 5, 5}, {1, 1, 1, 1}};
+  // s[3] is never initialised by the reference (std::fill over [s[0], s[3]), :43): zero
+  static const double s[4][4] = {{0, 0, 0.3, 0.3}, {0, 0, 0, 0}, {0.15, 0.15, 0, 0}, {0, 0, 0, 0}};
+  static const double fq[6] = {0, 10, 5, 2, 1, 0.01}, fqf[6] = {1, 20, 8, 3, 1, 0.01};
+  static const double fr[4][4] = {{0, 0, 0.01, 0.01}, {0, 0, 0, 0}, {0.01, 0.01, 0, 0}, {0, 0, 0, 0}};
+  for (int m = 0; m < 4; ++m) {
+    for (int i = 0; i < 14; ++i) {
+      w->wb_Q[m][i] = 0.01 * q[i];
+      w->wb_Qf[m][i] = 100 * qf[m][i];
+    }
+    for (int i = 0; i < 4; ++i) {
+      w->wb_R[m][i] = 0.5 * r[m][i];
+      w->wb_S[m][i] = s[m][i];
+      w->fb_R[m][i] = fr[m][i];
+    }
+    for (int i = 0; i < 6; ++i) {
+      w->fb_Q[m][i] = 0.01 * fq[i];
+      w->fb_Qf[m][i] = 100 * fqf[i];
+    }
+  }
+  return MHPC_OK;
+}
+
+// MHPCConstraints.cpp:14-88 (WBConstraint: b_torque 33, _friccoeff, initialize_AL_REB_PARAMS)
+extern "C" int mhpc_default_constraint_params(mhpc_constraint_params* c) {
+  if (!c) {
+    mhpc_g_err = "null argument";
+    return MHPC_ERR_INVALID;
+  }
+  c->torque_limit = 33;
+  c->friction_coeff = 0.5;
+  for (int m = 0; m < 4; ++m) {
+    c->sigma[m] = (m == 1 || m == 3) ? 5 : 0;
+    c->delta[m] = 0.1;
+    c->delta_min[m] = 0.01;
+    c->eps_torque[m] = 0.01;
+    c->eps_grf[m] = 0.01;
+  }
+  return MHPC_OK;
+}
+extern "C" int mhpc_set_cost_weights(mhpc_handle* h, const mhpc_cost_weights* w) {
+  FWD(set_cost_weights, w);
+}
+extern "C" int mhpc_get_cost_weights(mhpc_handle* h, mhpc_cost_weights* w) {
+  FWD(get_cost_weights, w);
+}
+extern "C" int mhpc_set_constraint_params(mhpc_handle* h, const mhpc_constraint_params* c) {
+  FWD(set_constraint_params, c);
+}
+extern "C" int mhpc_get_constraint_params(mhpc_handle* h, mhpc_constraint_params* c) {
+  FWD(get_constraint_params, c);
 }
 extern "C" void mhpc_destroy(mhpc_handle* h) {
   if (!h) return;

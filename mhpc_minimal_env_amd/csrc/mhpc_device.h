@@ -10,29 +10,8 @@ namespace MHPC_NS {
 
 constexpr real PI = real(3.141592653589793238);  // MHPC_CPPTypes.h:18
 
-// ---- cost weights (MHPCCost.cpp:24-75) ------------------------------------------------
-static __constant__ real cQwb[14] = {real(0.01) * 0, real(0.01) * 10, real(0.01) * 5, real(0.01) * 4, real(0.01) * 4, real(0.01) * 4,
-                                real(0.01) * 4, real(0.01) * 2, real(0.01) * 1, real(0.01) * real(.01), real(0.01) * 6, real(0.01) * 6,
-                                real(0.01) * 6, real(0.01) * 6};
-static __constant__ real cQfwb[4][14] = {
-    {100 * real(0.), 100 * real(20.), 100 * real(8.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(2.),
-     100 * real(0.01), 100 * real(5.), 100 * real(5.), 100 * real(0.01), 100 * real(0.01)},
-    {100 * real(0.), 100 * real(20.), 100 * real(8.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(2.),
-     100 * real(0.01), 100 * real(5.), 100 * real(5.), 100 * real(5.), 100 * real(5.)},
-    {100 * real(0.), 100 * real(20.), 100 * real(8.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(2.),
-     100 * real(0.01), 100 * real(0.01), 100 * real(0.01), 100 * real(5.), 100 * real(5.)},
-    {100 * real(0.), 100 * real(20.), 100 * real(8.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(3.), 100 * real(2.),
-     100 * real(0.01), 100 * real(5.), 100 * real(5.), 100 * real(5.), 100 * real(5.)}};
-static __constant__ real cRwb[4][4] = {{real(0.5) * 5, real(0.5) * 5, real(0.5) * 1, real(0.5) * 1},
-                                  {real(0.5) * 1, real(0.5) * 1, real(0.5) * 1, real(0.5) * 1},
-                                  {real(0.5) * 1, real(0.5) * 1, real(0.5) * 5, real(0.5) * 5},
-                                  {real(0.5) * 1, real(0.5) * 1, real(0.5) * 1, real(0.5) * 1}};
-// s[3] is uninitialised in the reference (MHPCCost.cpp:43 fills s[0..2]); zero here, as in
-// the oracle.  It can only offset the value of WB mode-4 running costs (y = 0 in flight).
-static __constant__ real cSwb[4][4] = {{0, 0, real(0.3), real(0.3)}, {0, 0, 0, 0}, {real(0.15), real(0.15), 0, 0}, {0, 0, 0, 0}};
-static __constant__ real cQfb[6] = {real(0.01) * 0, real(0.01) * 10, real(0.01) * 5, real(0.01) * 2, real(0.01) * 1, real(0.01) * real(0.01)};
-static __constant__ real cQffb[6] = {100 * real(1.), 100 * real(20.), 100 * real(8.), 100 * real(3.), 100 * real(1.), 100 * real(0.01)};
-static __constant__ real cRfb[4][4] = {{0, 0, real(0.01), real(0.01)}, {0, 0, 0, 0}, {real(0.01), real(0.01), 0, 0}, {0, 0, 0, 0}};
+// Cost weights and constraint parameters live in SolveParams::cw (mhpc_set_cost_weights /
+// mhpc_set_constraint_params; defaults MHPCCost.cpp:24-75, MHPCConstraints.cpp:14-88).
 // terminal WB state references (ReferenceGen.cpp:45-52), velocity entry filled at run time
 static __constant__ real cXtermWB[4][14] = {
     {0, -real(0.1432), -PI / 25, real(0.35) * PI, -real(0.65) * PI, real(0.35) * PI, -real(0.6) * PI, 0, 1, 0, 0, 0, 0, 0},
@@ -112,27 +91,28 @@ static __device__ real wb_running_cost(const SolveParams& sp, int mode, real dt,
   const real ry[4] = {0, kGRF, 0, kGRF};
   real l = 0, t = 0;
 #pragma unroll
-  for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; l += e * cQwb[i] * e; }
+  for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; l += e * sp.cw.wQ[m][i] * e; }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { const real e = u[i]; t += e * cRwb[m][i] * e; }
+  for (int i = 0; i < 4; ++i) { const real e = u[i]; t += e * sp.cw.wR[m][i] * e; }
   l += t;
   t = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { const real e = y[i] - ry[i]; t += e * cSwb[m][i] * e; }
+  for (int i = 0; i < 4; ++i) { const real e = y[i] - ry[i]; t += e * sp.cw.wS[m][i] * e; }
   l += t;
   l = l * dt;
   if (reb) {
     real B, Bz, Bzz;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {  // torque limits 33 -/+ u
-      const real g = (i < 4 ? -u[i] : u[i - 4]) + 33;
+    for (int i = 0; i < 8; ++i) {  // torque limits tq_lim -/+ u
+      const real g = (i < 4 ? -u[i] : u[i - 4]) + sp.cw.tq_lim;
       reduced_barrier(g, delta, &B, &Bz, &Bzz);
       l += eps_tq * B * dt;
     }
     // joint limits carry eps_ReB = 0 (MHPCConstraints.cpp:64-84): contribution 0 * B * dt
-    if (mode == 1 || mode == 3) {  // GRF: Fz >= 0, mu Fz -/+ Fx >= 0 with mu = 0.5
+    if (mode == 1 || mode == 3) {  // GRF: Fz >= 0, mu Fz -/+ Fx >= 0
       const int o = mode == 1 ? 2 : 0;
-      const real gs[3] = {y[o + 1], -y[o] + real(0.5) * y[o + 1], y[o] + real(0.5) * y[o + 1]};
+      const real mu = sp.cw.mu;
+      const real gs[3] = {y[o + 1], -y[o] + mu * y[o + 1], y[o] + mu * y[o + 1]};
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         reduced_barrier(gs[i], delta, &B, &Bz, &Bzz);
@@ -151,9 +131,9 @@ static __device__ real fb_running_cost(const SolveParams& sp, int mode, real dt,
   const real ru[4] = {0, kGRF, 0, kGRF};
   real l = 0, t = 0;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; l += e * cQfb[i] * e; }
+  for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; l += e * sp.cw.fQ[m][i] * e; }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { const real e = u[i] - ru[i]; t += e * cRfb[m][i] * e; }
+  for (int i = 0; i < 4; ++i) { const real e = u[i] - ru[i]; t += e * sp.cw.fR[m][i] * e; }
   l += t;
   l += real(0.0);  // S = 0 for the floating base (y = 0)
   return l * dt;
@@ -163,21 +143,22 @@ static __device__ real fb_running_cost(const SolveParams& sp, int mode, real dt,
 // the CALC_PARTIALS_ONLY branch of SinglePhase.cpp:219-249; joint limits carry eps_ReB = 0
 // and contribute exact zeros).  out = lu[4], luu[4] (diagonal), ly[2], lyy[4] where ly/lyy
 // are the entries of the stance foot's force slots (zero in flight).
-static __device__ void wb_cost_uy_derivs(int mode, real dt, const real* u, const real* y,
-                                         bool reb, real delta, real eps_tq, real eps_grf,
-                                         real* out) {
+static __device__ void wb_cost_uy_derivs(const SolveParams& sp, int mode, real dt, const real* u,
+                                         const real* y, bool reb, real delta, real eps_tq,
+                                         real eps_grf, real* out) {
   const int m = mode - 1;
+  const real tq = sp.cw.tq_lim, mu = sp.cw.mu;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    real lu = (2 * dt * cRwb[m][c]) * (u[c] - real(0.0));
-    real luu = 2 * dt * cRwb[m][c];
+    real lu = (2 * dt * sp.cw.wR[m][c]) * (u[c] - real(0.0));
+    real luu = 2 * dt * sp.cw.wR[m][c];
     if (reb) {
       real B, Bz, Bzz;
-      // constraint c: g = -u_c + 33 (gu = -1); constraint 4 + c: g = u_c + 33 (gu = +1)
-      reduced_barrier(-real(1.0) * u[c] + 33, delta, &B, &Bz, &Bzz);
+      // constraint c: g = -u_c + tq (gu = -1); constraint 4 + c: g = u_c + tq (gu = +1)
+      reduced_barrier(-real(1.0) * u[c] + tq, delta, &B, &Bz, &Bzz);
       lu += eps_tq * Bz * -real(1.0) * dt;
       luu += eps_tq * (-real(1.0) * Bzz * -real(1.0)) * dt;
-      reduced_barrier(real(1.0) * u[c] + 33, delta, &B, &Bz, &Bzz);
+      reduced_barrier(real(1.0) * u[c] + tq, delta, &B, &Bz, &Bzz);
       lu += eps_tq * Bz * real(1.0) * dt;
       luu += eps_tq * (real(1.0) * Bzz * real(1.0)) * dt;
     }
@@ -188,12 +169,12 @@ static __device__ void wb_cost_uy_derivs(int mode, real dt, const real* u, const
   if (mode == 1 || mode == 3) {
     const int o = mode == 1 ? 2 : 0;
     const real fx = mode == 1 ? y[2] : y[0], fz = mode == 1 ? y[3] : y[1];
-    const real s0 = cSwb[m][o], s1 = cSwb[m][o + 1];
+    const real s0 = sp.cw.wS[m][o], s1 = sp.cw.wS[m][o + 1];
     real ly0 = (2 * dt * s0) * (fx - real(0.0));
     real ly1 = (2 * dt * s1) * (fz - kGRF);
     real l00 = 2 * dt * s0, l01 = real(0.0), l10 = real(0.0), l11 = 2 * dt * s1;
     if (reb) {
-      const real rows[3][2] = {{0, 1}, {-1, real(0.5)}, {1, real(0.5)}};  // coefficients on (Fx, Fz)
+      const real rows[3][2] = {{0, 1}, {-1, mu}, {1, mu}};  // coefficients on (Fx, Fz)
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         real B, Bz, Bzz;

@@ -452,7 +452,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           real rx[14];
           wb_term_ref(sp, mode, refT, rx);
           real Phi = 0;
-          for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+          for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
           Phi = Phi * real(0.5);
           if (ntc_of(mode, true)) {
             h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           real rx[6];
           fb_term_ref(sp, refT, rx);
           real Phi = 0;
-          for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * cQffb[i] * e; }
+          for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
           V += Phi * real(0.5);
         }
         J += V;
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
       real rx[14];
       wb_term_ref(sp, mode, refpos[N - 1], rx);
       real Phi = 0;
-      for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * cQfwb[mode - 1][i] * ee; }
+      for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.wQf[mode - 1][i] * ee; }
       Phi = Phi * real(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
       real rx[6];
       fb_term_ref(sp, refpos[N - 1], rx);
       real Phi = 0;
-      for (int i = 0; i < 6; ++i) { const real ee = x[i] - rx[i]; Phi += ee * cQffb[i] * ee; }
+      for (int i = 0; i < 6; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.fQf[mode - 1][i] * ee; }
       V += Phi * real(0.5);
     }
     J += V;
@@ -670,10 +670,10 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* ph
       if (wb) {
         rxi = i == 0 ? pos : i == 1 ? sp.height : i == 2 ? real(0.0)
               : i < 7 ? cQjointBias[i - 3] : i == 7 ? sp.vel : real(0.0);
-        w2 = 2 * dt * cQwb[i];
+        w2 = 2 * dt * sp.cw.wQ[mode - 1][i];
       } else {
         rxi = i == 0 ? pos : i == 1 ? sp.height : i == 3 ? sp.vel : real(0.0);
-        w2 = 2 * dt * cQfb[i];
+        w2 = 2 * dt * sp.cw.fQ[mode - 1][i];
       }
       o[i] = w2 * (x[i] - rxi);
     }
@@ -691,7 +691,7 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* ph
       const real s = st->par_sigma[p], lam = st->par_lambda[p];
       real v[14];
       for (int i = 0; i < 14; ++i) {
-        v[i] = cQfwb[mode - 1][i] * (x[i] - rx[i]);
+        v[i] = sp.cw.wQf[mode - 1][i] * (x[i] - rx[i]);
         if (al) v[i] += 50 * (s * s / 2 * hx[i] * h + lam * hx[i]);
       }
       if (ntc_of(mode, true) && sp.AL_active) {  // trials of the last line search
@@ -709,7 +709,7 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* ph
     } else {
       real rx[6];
       fb_term_ref(sp, pos, rx);
-      for (int i = 0; i < 6; ++i) o[i] = cQffb[i] * (x[i] - rx[i]);
+      for (int i = 0; i < 6; ++i) o[i] = sp.cw.fQf[mode - 1][i] * (x[i] - rx[i]);
     }
   }
 }
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(256, MHPC_PAR_MINB) void k_partials(SolveParams sp,
     // running-cost derivatives of controls and contact forces at the nominal knot
     // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
     real c[14];
-    wb_cost_uy_derivs(mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
+    wb_cost_uy_derivs(sp, mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
                       st->eps_tq[p], st->eps_grf[p], c);
 #pragma unroll
     for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
@@ -897,7 +897,8 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
       st->sigma[p] *= up;
       if (st->reb_active && wb) {
         st->delta[p] *= sp.update_relax;
-        if (st->delta[p] < real(0.01)) st->delta[p] = real(0.01);
+        const real dmin = sp.cw.delta_min[sp.mode[p] - 1];
+        if (st->delta[p] < dmin) st->delta[p] = dmin;
         st->eps_tq[p] *= sp.update_ReB;
         st->eps_grf[p] *= sp.update_ReB;
       }
@@ -928,10 +929,12 @@ __device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int
   for (int p = 0; p < MAXP; ++p) {
     st->V[p] = 0; st->dV[p] = 0; st->h[p] = 0; st->lambda[p] = 0;
     const bool wb = p < sp.n_wb && p < sp.P;
-    st->sigma[p] = (wb && ntc_of(sp.mode[p], true)) ? real(5.0) : real(0.0);
-    st->delta[p] = real(0.1);
-    st->eps_tq[p] = real(0.01);
-    st->eps_grf[p] = real(0.01);
+    // AL_REB_PARAMETER of the phase's mode (MHPCConstraints.cpp:43-88, mhpc_set_constraint_params)
+    const int m = p < sp.P ? sp.mode[p] - 1 : 0;
+    st->sigma[p] = (wb && ntc_of(sp.mode[p], true)) ? sp.cw.sigma0[m] : real(0.0);
+    st->delta[p] = sp.cw.delta0[m];
+    st->eps_tq[p] = sp.cw.eps_tq0[m];
+    st->eps_grf[p] = sp.cw.eps_grf0[m];
   }
   st->status = MHPC_SOLVE_OK;
   // ReB flag as the options set it (what a sweep right after initialization() sees); the
@@ -1093,7 +1096,7 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
       real rx[14];
       wb_term_ref(sp, mode, refpos[ko + N - 1], rx);
       real Phi = 0;
-      for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; Phi += e * cQfwb[mode - 1][i] * e; }
+      for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
       Phi = Phi * real(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
@@ -1108,7 +1111,7 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
       real rx[6];
       fb_term_ref(sp, refpos[ko + N - 1], rx);
       real Phi = 0;
-      for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; Phi += e * cQffb[i] * e; }
+      for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
       V += Phi * real(0.5);
     }
     sV[p] = V;

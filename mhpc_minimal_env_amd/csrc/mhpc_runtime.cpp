@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cmath>
 #include <string>
 #include <algorithm>
 #include <vector>
@@ -112,12 +113,6 @@ struct Handle {
   };
   std::vector<SubStreams> subs;
   hipEvent_t evstart = nullptr;
-  // the solve's launch schedule captured as a HIP graph (MHPC_VARIANT_GRAPH), replayed while
-  // the parameters it was captured with (launch arguments by value, schedule) are unchanged
-  int graph_req = 0;
-  hipGraphExec_t gexec = nullptr;
-  SolveParams gsp;
-  int gfull = -1, gnsub = -1;
 };
 
 // Phase layout of a descriptor: modes, knot counts and offsets, partials work items.
@@ -224,6 +219,98 @@ static void free_bufs(Handle* h) {
   memset(&d, 0, sizeof d);
 }
 
+// Host (double) parameter structs <-> the kernels' parameter block (real).
+static void put_weights(CostParams& cw, const mhpc_cost_weights& w) {
+  for (int m = 0; m < 4; ++m) {
+    for (int i = 0; i < 14; ++i) {
+      cw.wQ[m][i] = (real)w.wb_Q[m][i];
+      cw.wQf[m][i] = (real)w.wb_Qf[m][i];
+    }
+    for (int i = 0; i < 4; ++i) {
+      cw.wR[m][i] = (real)w.wb_R[m][i];
+      cw.wS[m][i] = (real)w.wb_S[m][i];
+      cw.fR[m][i] = (real)w.fb_R[m][i];
+    }
+    for (int i = 0; i < 6; ++i) {
+      cw.fQ[m][i] = (real)w.fb_Q[m][i];
+      cw.fQf[m][i] = (real)w.fb_Qf[m][i];
+    }
+  }
+}
+static void get_weights(const CostParams& cw, mhpc_cost_weights& w) {
+  for (int m = 0; m < 4; ++m) {
+    for (int i = 0; i < 14; ++i) {
+      w.wb_Q[m][i] = cw.wQ[m][i];
+      w.wb_Qf[m][i] = cw.wQf[m][i];
+    }
+    for (int i = 0; i < 4; ++i) {
+      w.wb_R[m][i] = cw.wR[m][i];
+      w.wb_S[m][i] = cw.wS[m][i];
+      w.fb_R[m][i] = cw.fR[m][i];
+    }
+    for (int i = 0; i < 6; ++i) {
+      w.fb_Q[m][i] = cw.fQ[m][i];
+      w.fb_Qf[m][i] = cw.fQf[m][i];
+    }
+  }
+}
+static void put_constraints(CostParams& cw, const mhpc_constraint_params& c) {
+  cw.tq_lim = (real)c.torque_limit;
+  cw.mu = (real)c.friction_coeff;
+  for (int m = 0; m < 4; ++m) {
+    cw.sigma0[m] = (real)c.sigma[m];
+    cw.delta0[m] = (real)c.delta[m];
+    cw.delta_min[m] = (real)c.delta_min[m];
+    cw.eps_tq0[m] = (real)c.eps_torque[m];
+    cw.eps_grf0[m] = (real)c.eps_grf[m];
+  }
+}
+static void get_constraints(const CostParams& cw, mhpc_constraint_params& c) {
+  c.torque_limit = cw.tq_lim;
+  c.friction_coeff = cw.mu;
+  for (int m = 0; m < 4; ++m) {
+    c.sigma[m] = cw.sigma0[m];
+    c.delta[m] = cw.delta0[m];
+    c.delta_min[m] = cw.delta_min[m];
+    c.eps_torque[m] = cw.eps_tq0[m];
+    c.eps_grf[m] = cw.eps_grf0[m];
+  }
+}
+
+int api_set_cost_weights(Handle* h, const mhpc_cost_weights* w) {
+  if (!h || !w) return fail(MHPC_ERR_INVALID, "null argument");
+  const double* v = &w->wb_Q[0][0];
+  for (size_t i = 0; i < sizeof(mhpc_cost_weights) / sizeof(double); ++i)
+    if (!std::isfinite(v[i]) || v[i] < 0) return fail(MHPC_ERR_INVALID, "cost weights must be finite and >= 0");
+  put_weights(h->sp.cw, *w);
+  return MHPC_OK;
+}
+int api_get_cost_weights(Handle* h, mhpc_cost_weights* w) {
+  if (!h || !w) return fail(MHPC_ERR_INVALID, "null argument");
+  get_weights(h->sp.cw, *w);
+  return MHPC_OK;
+}
+int api_set_constraint_params(Handle* h, const mhpc_constraint_params* c) {
+  if (!h || !c) return fail(MHPC_ERR_INVALID, "null argument");
+  const double* v = &c->torque_limit;
+  for (size_t i = 0; i < sizeof(mhpc_constraint_params) / sizeof(double); ++i)
+    if (!std::isfinite(v[i])) return fail(MHPC_ERR_INVALID, "constraint parameters must be finite");
+  if (!(c->torque_limit > 0)) return fail(MHPC_ERR_INVALID, "torque_limit must be > 0");
+  for (int m = 0; m < 4; ++m) {
+    if (!(c->delta[m] > 0) || !(c->delta_min[m] > 0))
+      return fail(MHPC_ERR_INVALID, "delta and delta_min must be > 0");
+    if (c->sigma[m] < 0 || c->eps_torque[m] < 0 || c->eps_grf[m] < 0)
+      return fail(MHPC_ERR_INVALID, "sigma and the ReB weights must be >= 0");
+  }
+  put_constraints(h->sp.cw, *c);
+  return MHPC_OK;
+}
+int api_get_constraint_params(Handle* h, mhpc_constraint_params* c) {
+  if (!h || !c) return fail(MHPC_ERR_INVALID, "null argument");
+  get_constraints(h->sp.cw, *c);
+  return MHPC_OK;
+}
+
 int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int batch,
                            int device, Handle** out) {
   if (!out || !opt) return fail(MHPC_ERR_INVALID, "null argument");
@@ -273,6 +360,14 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   sp.eps9 = pow(0.1, 9);
   sp.AL_active = opt->AL_active ? 1 : 0;
   sp.ReB_active = opt->ReB_active ? 1 : 0;
+  {  // the reference's weights and constraint parameters until mhpc_set_* replaces them
+    mhpc_cost_weights w;
+    mhpc_constraint_params c;
+    mhpc_default_cost_weights(&w);
+    mhpc_default_constraint_params(&c);
+    put_weights(sp.cw, w);
+    put_constraints(sp.cw, c);
+  }
 
   DevBufs& d = h->d;
   memset(&d, 0, sizeof d);
@@ -555,18 +650,26 @@ static int solve_async(Handle* h) {
   if (nsub <= 1) {
     const SolveBlock k{h->sp, h->d, h->stream, h->stream2, h->evfork, h->evjoin};
     for (const SolveOp& op : ops)
-      if ((rc = issue_op(h, k, op))) return rc;
+      if ((rc = issue_op(h, k, op))) {
+        (void)hipStreamWaitEvent(h->stream, h->evjoin, 0);
+        return rc;
+      }
+    // a schedule whose last partials have no sweep after them (max_DDP_iter = 0) still
+    // joins the second stream back before the solve counts as done
+    HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
   } else {
     if ((rc = ensure_sub_streams(h, nsub))) return rc;
     HIPCHK(hipEventRecord(h->evstart, h->stream));
     std::vector<SolveBlock> blk(nsub);
-    const int bs = (h->sp.B + nsub - 1) / nsub;
+    // even partition: every block non-empty (sub_batches() <= B), sizes differ by <= 1
+    const int B = h->sp.B;
     for (int s = 0; s < nsub; ++s) {
       const Handle::SubStreams& ss = h->subs[s];
       SolveBlock& k = blk[s];
+      const int b0 = (int)((int64_t)s * B / nsub), b1 = (int)((int64_t)(s + 1) * B / nsub);
       k.sp = h->sp;
-      k.sp.B = std::min(bs, h->sp.B - s * bs);
-      k.d = block_bufs(h->d, h->sp, (size_t)s * bs);
+      k.sp.B = b1 - b0;
+      k.d = block_bufs(h->d, h->sp, (size_t)b0);
       k.s1 = ss.s1;
       k.s2 = ss.s2;
       k.fork = ss.fork;
@@ -578,60 +681,38 @@ static int solve_async(Handle* h) {
     int lag = 1;
     if (const char* e = getenv("MHPC_SUB_LAG")) lag = atoi(e);  // tuning only
     lag = std::max(0, std::min(lag, nops - 1));
-    for (int t = 0; t < nops + (nsub - 1) * lag; ++t)
+    // every block's streams are joined back to h->stream even when an issue fails partway,
+    // so later work on the handle never races with a block's queued launches
+    auto join_all = [&]() -> hipError_t {
+      hipError_t e = hipSuccess;
       for (int s = 0; s < nsub; ++s) {
+        hipError_t e1 = hipStreamWaitEvent(blk[s].s1, blk[s].join, 0);
+        if (e1 == hipSuccess) e1 = hipEventRecord(h->subs[s].done, blk[s].s1);
+        if (e1 == hipSuccess) e1 = hipStreamWaitEvent(h->stream, h->subs[s].done, 0);
+        if (e == hipSuccess) e = e1;
+      }
+      return e;
+    };
+    rc = MHPC_OK;
+    for (int t = 0; t < nops + (nsub - 1) * lag && !rc; ++t)
+      for (int s = 0; s < nsub && !rc; ++s) {
         const int i = t - s * lag;
         if (i < 0 || i >= nops) continue;
-        if (s > 0 && i == 0 && lag > 0) HIPCHK(hipStreamWaitEvent(blk[s].s1, h->subs[s - 1].gate, 0));
-        if ((rc = issue_op(h, blk[s], ops[i]))) return rc;
-        if (s + 1 < nsub && lag > 0 && i == lag - 1) HIPCHK(hipEventRecord(h->subs[s].gate, blk[s].s1));
+        if (s > 0 && i == 0 && lag > 0 &&
+            hipStreamWaitEvent(blk[s].s1, h->subs[s - 1].gate, 0) != hipSuccess)
+          rc = fail(MHPC_ERR_DEVICE, "sub-batch gate wait failed");
+        if (!rc) rc = issue_op(h, blk[s], ops[i]);
+        if (!rc && s + 1 < nsub && lag > 0 && i == lag - 1 &&
+            hipEventRecord(h->subs[s].gate, blk[s].s1) != hipSuccess)
+          rc = fail(MHPC_ERR_DEVICE, "sub-batch gate record failed");
       }
-    for (int s = 0; s < nsub; ++s) {
-      HIPCHK(hipEventRecord(h->subs[s].done, blk[s].s1));
-      HIPCHK(hipStreamWaitEvent(h->stream, h->subs[s].done, 0));
-    }
+    const hipError_t ej = join_all();
+    if (rc) return rc;
+    HIPCHK(ej);
   }
   // batch totals of the per-problem counters (tiny reduction, NCNT words back)
   HIPCHK(hipMemsetAsync(h->dcnt, 0, NCNT * sizeof(unsigned long long), h->stream));
   HIPCHK(launch_reduce_counters(h->sp, h->d, h->dcnt, h->stream));
-  return MHPC_OK;
-}
-
-// The solve schedule as a HIP graph: ~35 dependent launches (two streams) replayed by the
-// device without a host round trip per launch.  Captured on first use and again whenever
-// the launch arguments (SolveParams by value), the schedule (real first rollout after
-// update_problem) or the sub-batch count change; not while per-launch profiling events are
-// requested (those need the host-issued schedule).
-static void drop_graph(Handle* h) {
-  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-  h->gexec = nullptr;
-}
-static int solve_graph(Handle* h) {
-  const int nsub = sub_batches(h);
-  const bool same = h->gexec && h->gfull == (h->need_full ? 1 : 0) && h->gnsub == nsub &&
-                    memcmp(&h->gsp, &h->sp, sizeof(SolveParams)) == 0;
-  if (!same) {
-    drop_graph(h);
-    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    int rc = solve_async(h);
-    hipGraph_t g = nullptr;
-    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
-    if (rc) {
-      if (g) (void)hipGraphDestroy(g);
-      return rc;
-    }
-    if (ec != hipSuccess) return fail(MHPC_ERR_DEVICE, std::string("graph capture: ") + hipGetErrorString(ec));
-    const hipError_t ei = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (ei != hipSuccess) {
-      h->gexec = nullptr;
-      return fail(MHPC_ERR_DEVICE, std::string("graph instantiate: ") + hipGetErrorString(ei));
-    }
-    memcpy(&h->gsp, &h->sp, sizeof(SolveParams));
-    h->gfull = h->need_full ? 1 : 0;
-    h->gnsub = nsub;
-  }
-  HIPCHK(hipGraphLaunch(h->gexec, h->stream));
   return MHPC_OK;
 }
 
@@ -643,12 +724,7 @@ int api_solve(Handle* h, int32_t* status) {
     return fail(MHPC_ERR_STATE, "x0 changed: call mhpc_initialize or mhpc_update_problem first");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
-  // Off unless requested: replaying the schedule measured no faster than issuing it (the gaps
-  // between dependent kernels are device-side; profiles/r02_ab_graph.txt).  Never with
-  // sub-batches: a solve captured with their four-stream fan-out segfaulted on the host in
-  // the sub-batch parity test (sub-batching is off by default, profiles/r02_ab_subbatch.txt).
-  const bool graph = h->graph_req == MHPC_VARIANT_GRAPH_ON && !h->profile && sub_batches(h) <= 1;
-  int rc = graph ? solve_graph(h) : solve_async(h);
+  int rc = solve_async(h);
   if (rc) return rc;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   HIPCHK(hipMemcpyAsync(h->cnt, h->dcnt, NCNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -680,29 +756,33 @@ int api_solve(Handle* h, int32_t* status) {
 
 // Rows [ko, ko + N) of a problem-major [B][NK][per] device array into buf ([B][N][per]):
 // one strided copy of just the requested phase (not the whole trajectory buffer).
-static int copy_rows(Handle* h, const real* src, int per, int ko, int N, std::vector<real>& buf) {
-  const size_t B = h->sp.B, NK = h->sp.NK, w = (size_t)N * per * sizeof(real);
+static int copy_rows(Handle* h, const real* src, int per, int ko, int N, size_t b0, size_t B,
+                     std::vector<real>& buf) {
+  const size_t NK = h->sp.NK, w = (size_t)N * per * sizeof(real);
   buf.resize(B * N * per);
-  HIPCHK(hipMemcpy2DAsync(buf.data(), w, src + (size_t)ko * per, NK * per * sizeof(real), w, B,
-                          hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpy2DAsync(buf.data(), w, src + (b0 * NK + (size_t)ko) * per,
+                          NK * per * sizeof(real), w, B, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return MHPC_OK;
 }
 
-int api_get_phase(Handle* h, int phase, double* x, double* u, double* y,
-                              double* K, double* du, double* Vx) {
+// Problems [first, first + count) of one phase (count = batch: mhpc_get_phase).
+int api_get_phase(Handle* h, int phase, int first, int count, double* x, double* u, double* y,
+                  double* K, double* du, double* Vx) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
   if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
   const SolveParams& sp = h->sp;
   if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
+  if (first < 0 || count < 1 || first > sp.B - count)
+    return fail(MHPC_ERR_INVALID, "problem range outside the batch");
   HIPCHK(hipSetDevice(h->device));
-  const size_t B = sp.B;
+  const size_t B = count, b0 = first;
   const int n = sp.xs[phase], N = sp.N[phase], ko = sp.ko[phase];
   std::vector<real> buf;
   int rc;
   if (x || u || y) {
     HIPCHK(launch_export(sp, h->d, h->stream));
-    if ((rc = copy_rows(h, h->d.out, KS, ko, N, buf))) return rc;
+    if ((rc = copy_rows(h, h->d.out, KS, ko, N, b0, B, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k) {
         const real* r = &buf[(b * N + k) * KS];
@@ -715,17 +795,17 @@ int api_get_phase(Handle* h, int phase, double* x, double* u, double* y,
       }
   }
   if (K) {
-    if ((rc = copy_rows(h, h->d.K, 56, ko, N, buf))) return rc;
+    if ((rc = copy_rows(h, h->d.K, 56, ko, N, b0, B, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
         for (int i = 0; i < 4 * n; ++i) K[(b * N + k) * 4 * n + i] = buf[(b * N + k) * 56 + i];
   }
   if (du) {
-    if ((rc = copy_rows(h, h->d.du, 4, ko, N, buf))) return rc;
+    if ((rc = copy_rows(h, h->d.du, 4, ko, N, b0, B, buf))) return rc;
     for (size_t i = 0; i < B * N * 4; ++i) du[i] = buf[i];
   }
   if (Vx) {
-    if ((rc = copy_rows(h, h->d.G, 14, ko, N, buf))) return rc;
+    if ((rc = copy_rows(h, h->d.G, 14, ko, N, b0, B, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k)
         for (int i = 0; i < n; ++i) Vx[(b * N + k) * n + i] = buf[(b * N + k) * 14 + i];
@@ -891,6 +971,8 @@ int api_update_problem(Handle* h, const mhpc_gait* gait) {
   return MHPC_OK;
 }
 
+int api_batch(Handle* h) { return h ? h->sp.B : 0; }
+
 int api_get_desc(Handle* h, mhpc_problem_desc* desc) {
   if (!h || !desc) return fail(MHPC_ERR_INVALID, "null argument");
   *desc = h->desc;
@@ -940,11 +1022,6 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
     sp.var_overlap = variant;
     return MHPC_OK;
   }
-  if (which == MHPC_VARIANT_GRAPH) {
-    if (variant < 0 || variant > MHPC_VARIANT_GRAPH_OFF) return fail(MHPC_ERR_INVALID, "no such graph variant");
-    h->graph_req = variant;
-    return MHPC_OK;
-  }
   if (which == MHPC_VARIANT_SUBBATCH) {
     if (variant < 0 || variant > MHPC_MAX_SUBBATCH) return fail(MHPC_ERR_INVALID, "sub-batch count must be 0..4");
     h->nsub_req = variant;
@@ -980,7 +1057,6 @@ void api_destroy(Handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  drop_graph(h);
   free_bufs(h);
   if (h->dcnt) (void)hipFree(h->dcnt);
   if (h->store) (void)hipFree(h->store);

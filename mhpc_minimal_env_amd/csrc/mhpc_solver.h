@@ -43,6 +43,13 @@ enum {
   NCNT
 };
 
+struct CostParams {
+  real wQ[4][14], wR[4][4], wS[4][4], wQf[4][14];  // whole-body phases
+  real fQ[4][6], fR[4][4], fQf[4][6];              // SRB phases
+  real tq_lim, mu;                                 // torque limit, GRF friction coefficient
+  real sigma0[4], delta0[4], delta_min[4], eps_tq0[4], eps_grf0[4];  // AL / ReB initial values
+};
+
 struct SolveParams {
   int B, P, n_wb, NK;
   int mode[MAXP], N[MAXP], ko[MAXP], xs[MAXP];
@@ -62,6 +69,10 @@ struct SolveParams {
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
   int ncu, var_bws, var_ro, var_overlap;
+  // cost weights (diagonals per mode, CostBase.h:9-46 / MHPCCost.cpp:24-75) and constraint
+  // parameters (ConstraintsBase.h:11-50 / MHPCConstraints.cpp:14-88): mhpc_set_cost_weights /
+  // mhpc_set_constraint_params; read by every kernel from its parameter block
+  CostParams cw;
 };
 
 struct ProbState {
@@ -120,17 +131,6 @@ struct DevBufs {
   ProbState* st;
   real* out;    // export staging [B][NK][KS]
   BwsCarry* carry;  // [B]
-};
-
-// ---- cost weights (MHPCCost.cpp:24-75) and constraint constants (MHPCConstraints.cpp) --
-#if defined(__HIPCC__)
-#define MHPC_CONST __constant__
-#else
-#define MHPC_CONST static const
-#endif
-
-struct Weights {
-  real Q[4][14], R[4][4], S[4][4], Qf[4][14];
 };
 
 }  // namespace MHPC_NS

@@ -206,6 +206,45 @@ def random_x0(batch: int, seed: int = X0_SEED, offset: int = 0) -> np.ndarray:
 
 
 # ----------------------------------------------------------------------------------------
+class SinglePhaseView:
+    """One phase of the batch after a solve, with the public members of the reference's
+    SinglePhaseAbstract (SinglePhaseAbstract.h:66-134): _modeidx, _phaseidx, _dt,
+    _N_TIMESTEPS, _xsize/_usize/_ysize, and _V / _dV (phase cost, expected change) as
+    [batch] arrays; get_nominal_ms_ptr() / get_CTG_info_ptr() return the phase's nominal
+    (x, u, y) and cost-to-go (G = Vx, du, K) arrays [batch][N][...] (MHPC_CompoundTypes.h:7-22,
+    88-101).  Read lazily from the device; valid until the next solve / update_problem."""
+
+    def __init__(self, loco: "MHPCLocomotion", p: int):
+        d = loco.desc
+        self._loco, self._phaseidx = loco, p
+        self._modeidx = int(d.mode_seq[p])
+        self._N_TIMESTEPS = int(d.N[p])
+        self._xsize, self._usize, self._ysize = d.xsize(p), 4, 4
+        self._dt = float(d.dt_wb if p < d.n_wb else d.dt_fb)
+
+    def get_modeidx(self) -> int:
+        return self._modeidx
+
+    @property
+    def _V(self) -> np.ndarray:
+        return self._loco.get_scalars()["V"][:, self._phaseidx]
+
+    @property
+    def _dV(self) -> np.ndarray:
+        return self._loco.get_scalars()["dV"][:, self._phaseidx]
+
+    def get_nominal_ms_ptr(self) -> dict:
+        q = self._loco.get_phase(self._phaseidx)
+        return {"x": q["x"], "u": q["u"], "y": q["y"]}
+
+    def get_CTG_info_ptr(self) -> dict:
+        q = self._loco.get_phase(self._phaseidx)
+        return {"G": q["Vx"], "du": q["du"], "K": q["K"]}
+
+    def get_terminal_state(self) -> np.ndarray:
+        return self.get_nominal_ms_ptr()["x"][:, -1, :]
+
+
 class MHPCLocomotion:
     """Batched MHPCLocomotion<double> over the C-ABI.
 
@@ -265,6 +304,53 @@ class MHPCLocomotion:
         d = capi.ProblemDesc()
         capi.check(L.mhpc_get_desc(self._h, __import__("ctypes").byref(d)), "mhpc_get_desc")
         self.desc = d
+
+    # MultiPhaseDDP's public members (MultiPhaseDDP.h:12-63), batched: [batch] arrays
+    @property
+    def _phases(self):
+        return [SinglePhaseView(self, p) for p in range(self.desc.n_phases)]
+
+    @property
+    def _n_phases(self) -> int:
+        return self.desc.n_phases
+
+    @property
+    def _actual_cost(self) -> np.ndarray:
+        return self.get_scalars()["J"]
+
+    @property
+    def _exp_cost_change(self) -> np.ndarray:
+        return self.get_scalars()["dV_exp"]
+
+    @property
+    def _tconstr_violation(self) -> np.ndarray:
+        return self.get_scalars()["viol"]
+
+    # -- cost / constraint parameters (CostBase.h:9-46, ConstraintsBase.h:11-50) -----------
+    def set_cost_weights(self, w: "capi.CostWeights"):
+        """Replace the diagonal cost weights (MHPCCost.cpp:24-75 values by default) for every
+        later solve of this handle (mhpc_set_cost_weights)."""
+        capi.check(capi.lib().mhpc_set_cost_weights(self._h, __import__("ctypes").byref(w)),
+                   "mhpc_set_cost_weights")
+
+    def get_cost_weights(self) -> "capi.CostWeights":
+        w = capi.CostWeights()
+        capi.check(capi.lib().mhpc_get_cost_weights(self._h, __import__("ctypes").byref(w)),
+                   "mhpc_get_cost_weights")
+        return w
+
+    def set_constraint_params(self, c: "capi.ConstraintParams"):
+        """Replace torque limit, friction coefficient and the AL / ReB initial parameters
+        (MHPCConstraints.cpp:14-88 values by default); the initial values take effect at the
+        next initialization() / update_problem() (mhpc_set_constraint_params)."""
+        capi.check(capi.lib().mhpc_set_constraint_params(self._h, __import__("ctypes").byref(c)),
+                   "mhpc_set_constraint_params")
+
+    def get_constraint_params(self) -> "capi.ConstraintParams":
+        c = capi.ConstraintParams()
+        capi.check(capi.lib().mhpc_get_constraint_params(self._h, __import__("ctypes").byref(c)),
+                   "mhpc_get_constraint_params")
+        return c
 
     def get_exec(self) -> dict:
         """Execution horizon of solve_mhpc (MHPCLocomotion.cpp:176-194): the nominal and
@@ -344,15 +430,13 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
     def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto",
-                           sub_batches: int = 0, graph: str = "auto"):
+                           sub_batches: int = 0):
         """Pin the backward-sweep / line-search launch variant, the partials / sweep
-        overlap, the number of concurrently scheduled sub-batches and whether the solve
-        schedule replays as a HIP graph (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
+        overlap and the number of concurrently scheduled sub-batches
+        (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
         capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by batch size and phase layout."""
         L = capi.lib()
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SUBBATCH, int(sub_batches)),
-                   "mhpc_set_kernel_variant")
-        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_GRAPH, capi.GRAPH_VARIANTS[graph]),
                    "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_OVERLAP,
                                              capi.OVERLAP_VARIANTS[overlap]), "mhpc_set_kernel_variant")

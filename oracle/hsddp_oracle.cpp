@@ -257,8 +257,19 @@ Weights make_fb_weights() {
   return w;
 }
 
-const Weights kWB = make_wb_weights();
-const Weights kFB = make_fb_weights();
+// The solve's weights: the reference's values unless oracle_set_params replaced them (the
+// counterpart of mhpc_set_cost_weights: the reference's Cost objects with other diagonals)
+Weights kWB = make_wb_weights();
+Weights kFB = make_fb_weights();
+
+// Constraint parameters (MHPCConstraints.cpp:14-88; mhpc_set_constraint_params counterpart)
+struct ConParams {
+  double tq_lim = 33, mu = 0.5;
+  double sigma[4] = {0, 5, 0, 5}, delta[4] = {0.1, 0.1, 0.1, 0.1},
+         delta_min[4] = {0.01, 0.01, 0.01, 0.01}, eps_tq[4] = {0.01, 0.01, 0.01, 0.01},
+         eps_grf[4] = {0.01, 0.01, 0.01, 0.01};
+};
+ConParams kCon;
 
 struct Phase {
   bool wb;
@@ -445,7 +456,7 @@ void path_constraint(Phase& ph, const Knot& s) {
   for (int i = 0; i < 8; ++i) {  // torque_limit
     Ineq& c = ph.pc[i];
     const double sgn = i < 4 ? -1.0 : 1.0;
-    c.g = sgn * s.u[i % 4] + 33;
+    c.g = sgn * s.u[i % 4] + kCon.tq_lim;
     c.gu[i % 4] = sgn;
   }
   for (int i = 0; i < 8; ++i) {  // joint_limit
@@ -455,7 +466,7 @@ void path_constraint(Phase& ph, const Knot& s) {
     c.gx[3 + i % 4] = sgn;
   }
   if (ph.mode == 1 || ph.mode == 3) {  // GRF_constraint
-    const double mu = 0.5;
+    const double mu = kCon.mu;
     const int o = ph.mode == 1 ? 2 : 0;  // back foot force in y[2:4], front in y[0:2]
     double rows[3][4] = {{0}};
     rows[0][o + 1] = 1;
@@ -900,13 +911,14 @@ void init_params(Phase& ph) {  // WBConstraint ctor / initialize_AL_REB_PARAMS (
   ph.npc = (m == 1 || m == 3) ? 19 : 16;
   ph.ntc = (m == 2 || m == 4) ? 1 : 0;
   for (int i = 0; i < ph.npc; ++i) {
-    ph.delta[i] = 0.1;
-    ph.delta_min[i] = 0.01;
-    ph.eps_reb[i] = (i >= 8 && i < 16) ? 0.0 : 0.01;
+    ph.delta[i] = kCon.delta[m - 1];
+    ph.delta_min[i] = kCon.delta_min[m - 1];
+    // torque limits 0..7, joint limits 8..15 (eps_ReB 0), GRF 16..18
+    ph.eps_reb[i] = i < 8 ? kCon.eps_tq[m - 1] : i < 16 ? 0.0 : kCon.eps_grf[m - 1];
   }
   ph.reb_empty = false;
   if (m == 2 || m == 4) {
-    ph.sigma = 5;
+    ph.sigma = kCon.sigma[m - 1];
     ph.al_empty = false;
   }
 }
@@ -1126,6 +1138,43 @@ extern "C" int oracle_riccati_knot(int n, const double* A, const double* B, cons
 
 // Eigen::LDLT(A).isPositive() as the oracle restates it (row-major 4x4); tests only.
 extern "C" int oracle_ldlt_is_positive(const double* A) { return ldlt_is_positive(A, 4) ? 1 : 0; }
+
+// Counterpart of mhpc_set_cost_weights / mhpc_set_constraint_params for later oracle calls
+// (NULL restores the reference's values); not thread-safe against a running solve.
+extern "C" int oracle_set_params(const mhpc_cost_weights* w, const mhpc_constraint_params* c) {
+  kWB = make_wb_weights();
+  kFB = make_fb_weights();
+  if (w) {
+    for (int m = 0; m < 4; ++m) {
+      for (int i = 0; i < 14; ++i) {
+        kWB.Q[m][i] = w->wb_Q[m][i];
+        kWB.Qf[m][i] = w->wb_Qf[m][i];
+      }
+      for (int i = 0; i < 4; ++i) {
+        kWB.R[m][i] = w->wb_R[m][i];
+        kWB.S[m][i] = w->wb_S[m][i];
+        kFB.R[m][i] = w->fb_R[m][i];
+      }
+      for (int i = 0; i < 6; ++i) {
+        kFB.Q[m][i] = w->fb_Q[m][i];
+        kFB.Qf[m][i] = w->fb_Qf[m][i];
+      }
+    }
+  }
+  kCon = ConParams();
+  if (c) {
+    kCon.tq_lim = c->torque_limit;
+    kCon.mu = c->friction_coeff;
+    for (int m = 0; m < 4; ++m) {
+      kCon.sigma[m] = c->sigma[m];
+      kCon.delta[m] = c->delta[m];
+      kCon.delta_min[m] = c->delta_min[m];
+      kCon.eps_tq[m] = c->eps_torque[m];
+      kCon.eps_grf[m] = c->eps_grf[m];
+    }
+  }
+  return 0;
+}
 
 extern "C" int oracle_load_ref(const char* path) {
   if (g_ref.handle) return 0;

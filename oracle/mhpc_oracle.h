@@ -14,6 +14,10 @@ extern "C" {
 /* Load the CasADi reference kernels from `path` (oracle/_ref/libmhpc_casadi_ref.so). */
 int oracle_load_ref(const char* path);
 
+/* Cost weights / constraint parameters for later calls (counterpart of
+ * mhpc_set_cost_weights / mhpc_set_constraint_params); NULL = the reference's values. */
+int oracle_set_params(const mhpc_cost_weights* w, const mhpc_constraint_params* c);
+
 /* Solve `batch` independent problems (x0: [batch][xsize of phase 0]).
  * do_solve = 0 runs initialization only (refs + PD warm start), leaving the nominal
  * trajectory of the warm start in the outputs.

@@ -85,6 +85,17 @@ def solve(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray, nthread
     return out
 
 
+def set_params(weights=None, constraints=None):
+    """Cost weights / constraint parameters (capi.CostWeights / capi.ConstraintParams) for
+    later oracle calls; None = the reference's values (oracle_set_params)."""
+    L = lib()
+    L.oracle_set_params.restype = ctypes.c_int
+    rc = L.oracle_set_params(ctypes.byref(weights) if weights is not None else None,
+                             ctypes.byref(constraints) if constraints is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle_set_params failed ({rc})")
+
+
 def rollout_costs(desc: capi.ProblemDesc, opt: capi.HsddpOption, x0: np.ndarray, eps,
                   nthreads: int = 1, do_solve: bool = True) -> dict:
     """forward_sweep_dynamics_only at every step size in `eps` from the state the solve

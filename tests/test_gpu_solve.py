@@ -135,3 +135,78 @@ def test_reference_demo_cpp_driver(need_gpu, tmp_path):
     assert abs(J - ref["J"][0]) <= 1e-8 * max(1.0, abs(ref["J"][0]))
     got = run_gpu(desc, L.HSDDP_OPTION(), L.X0_DEFAULT[None, :].copy())
     compare(got, ref)
+    # the per-phase surface (_phases[p]->_V, _dV, _N_TIMESTEPS, get_modeidx(),
+    # get_nominal_ms_ptr(), get_CTG_info_ptr()) as the driver read it, vs the oracle
+    cat = {k: [] for k in ("X", "U", "Y", "G", "DU", "K")}
+    V, dV = [], []
+    rows = (tmp_path / "phases.txt").read_text().strip().split("\n")
+    i, p = 0, 0
+    while i < len(rows):
+        h = rows[i].split()
+        assert int(h[1]) == p and int(h[3]) == desc.mode_seq[p]
+        N, n = int(h[5]), desc.xsize(p)
+        assert N == desc.N[p]
+        V.append(float(h[7]))
+        dV.append(float(h[9]))
+        a = np.array([[float(v) for v in r.split()] for r in rows[i + 1:i + 1 + N]])
+        assert a.shape == (N, 2 * n + 12 + 4 * n)
+        for k, (lo, w) in (("X", (0, n)), ("U", (n, 4)), ("Y", (n + 4, 4)), ("G", (n + 8, n)),
+                           ("DU", (2 * n + 8, 4)), ("K", (2 * n + 12, 4 * n))):
+            cat[k].append(a[:, lo:lo + w].reshape(-1))
+        i += 1 + N
+        p += 1
+    assert p == desc.n_phases
+    for k in cat:
+        a, b = np.concatenate(cat[k]), np.asarray(ref[k][0], float)
+        assert a.shape == b.shape, k
+        assert float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)))) <= SOLVE_TOL, k
+    for k, a in (("V", V), ("dV", dV)):
+        b = np.asarray(ref[k][0], float)
+        assert float(np.max(np.abs(np.array(a) - b) / np.maximum(1.0, np.abs(b)))) <= SOLVE_TOL, k
+
+
+def test_phase_views_and_problem_range(need_gpu):
+    """The reference's per-phase surface in the Python mirror (_phases[p]._V / _dV /
+    _N_TIMESTEPS / get_nominal_ms_ptr / get_CTG_info_ptr, SinglePhaseAbstract.h:79-81,116-119)
+    and mhpc_get_phase_problems (one problem's phase) agree with the batch-wide exports and
+    the oracle; a range outside the batch is rejected."""
+    import ctypes
+    from mhpc_minimal_env_amd import capi, configs, locomotion as L
+    desc, opt = configs.c3_desc(), L.HSDDP_OPTION()
+    x0 = configs.x0_for(desc, 5, offset=77)
+    loco = L.MHPCLocomotion(desc=desc, option=opt, batch=5, device=0)
+    try:
+        loco.set_initial_condition(x0)
+        loco.initialization()
+        loco.solve_mhpc()
+        sc = loco.get_scalars()
+        assert loco._n_phases == desc.n_phases
+        np.testing.assert_array_equal(loco._actual_cost, sc["J"])
+        for p, ph in enumerate(loco._phases):
+            assert ph._N_TIMESTEPS == desc.N[p] and ph.get_modeidx() == desc.mode_seq[p]
+            np.testing.assert_array_equal(ph._V, sc["V"][:, p])
+            np.testing.assert_array_equal(ph._dV, sc["dV"][:, p])
+            full = loco.get_phase(p)
+            np.testing.assert_array_equal(ph.get_nominal_ms_ptr()["x"], full["x"])
+            np.testing.assert_array_equal(ph.get_CTG_info_ptr()["K"], full["K"])
+            n, N = desc.xsize(p), desc.N[p]
+            one = {k: np.zeros(s) for k, s in (("x", (N, n)), ("u", (N, 4)), ("y", (N, 4)),
+                                                ("K", (N, 4, n)), ("du", (N, 4)), ("Vx", (N, n)))}
+            capi.check(capi.lib().mhpc_get_phase_problems(
+                loco._h, p, 3, 1, *[capi.dptr(one[k]) for k in ("x", "u", "y", "K", "du", "Vx")]),
+                "mhpc_get_phase_problems")
+            for k in one:
+                np.testing.assert_array_equal(one[k], full[k][3], err_msg=f"phase {p} {k}")
+        buf = np.zeros(10000)
+        for first, count in ((4, 2), (-1, 1), (0, 0)):
+            assert capi.lib().mhpc_get_phase_problems(loco._h, 0, first, count, capi.dptr(buf),
+                                                      None, None, None, None, None) == capi.MHPC_ERR_INVALID
+        got = {"V": sc["V"], "dV": sc["dV"]}
+    finally:
+        loco.close()
+    O = _oracle()
+    if O is None:
+        pytest.skip("oracle not built")
+    ref = O.solve(desc, opt.to_c(), x0, nthreads=5)
+    for k in ("V", "dV"):
+        assert rel_err(got[k], ref[k]) <= SOLVE_TOL, k
