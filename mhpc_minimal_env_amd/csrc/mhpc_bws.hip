@@ -19,6 +19,8 @@
 // registers while knot k computes, and dropped into LDS at the top of the next knot.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mhpc_device.h"
 
 namespace MHPC_NS {
@@ -73,6 +75,16 @@ template <int NX> struct QShape {
   static constexpr int QV = QS - 1;
 };
 
+// Arithmetic type of the 4x4 control block of a knot (adjugate, determinant, Quu^-1, the
+// gains tq = Qux' Quu^-1 and the products that update H / G / dV with them): the solve's
+// type, or double in an fp32 build with MHPC_BWS_WIDE (the fp32 sweep's gains then carry the
+// rounding of the fp32 Q blocks only, not of an fp32 inversion).
+#if defined(MHPC_FP32) && MHPC_BWS_WIDE
+using wreal = double;
+#else
+using wreal = real;
+#endif
+
 struct BwsLds {
   alignas(16) real H[196];
   alignas(16) real G[14];  // value function of knot k+1, then of knot k (row stride NX)
@@ -96,10 +108,10 @@ struct BwsLds {
   real Qv[18];         // (Qx, Qu)
   real xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
   alignas(16) real Kst[56];          // results of the last knot, stored one knot later
-  alignas(16) real inv[16];          // Quu^-1 (unsymmetrised), broadcast through LDS
+  alignas(16) wreal inv[16];         // Quu^-1 (unsymmetrised), broadcast through LDS
   alignas(16) real dust[4];
   real hx[14], Hs[9], G2v[14];
-  real junk[64];       // write target of the spare lanes of a round (never read)
+  alignas(16) real junk[64];  // write target of the spare lanes of a round (never read)
   real dV;
   int fail;
 #ifdef MHPC_BWS_TIMING
@@ -416,10 +428,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
   // spread over lanes 0..15 (one 3x3 minor each) and broadcast back with readlane (no LDS
   // round trip); then, in the same round, tq = Qux' Quu_inv, K = -tq', du, dV and
   // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
-  real q0[4];
+  wreal q0[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) q0[c] = qu(sh, QS, NX, 0, NX + c);
-  real adj = real(0.0);
+  wreal adj = wreal(0.0);
   bool psd;
   {
     // the PSD verdict is applied at the end of the round: a failed knot abandons the sweep
@@ -428,9 +440,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
 #define QM(r, c) qu(sh, QS, NX, r, NX + (c))
-    const real m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
-    const real m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
-    const real m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
+    const wreal m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
+    const wreal m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
+    const wreal m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
 #undef QM
     real A[16];
 #pragma unroll
@@ -446,16 +458,16 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     psd = ldlt_is_positive4(A);
 #endif
     // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
-    const real det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
-                        m02 * (m10 * m21 - m11 * m20);
+    const wreal det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
+                         m02 * (m10 * m21 - m11 * m20);
     adj = ((i + j) & 1) ? -det3 : det3;
   }
-  const real det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
-                     q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
-  const real invl = adj / det;
-  real Qi[16];
+  const wreal det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
+                      q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
+  const wreal invl = adj / det;
+  wreal Qi[16];
   {
-    real inv[16];  // unsymmetrised inverse (uniform)
+    wreal inv[16];  // unsymmetrised inverse (uniform)
 #if MHPC_BWS_INVLDS
     // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
     // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
@@ -468,7 +480,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
 #ifndef MHPC_BWS_WAVEBAR
 #define MHPC_BWS_WAVEBAR 0
 #endif
-    *(lane < 16 ? &sh.inv[lane] : &sh.junk[lane & 63]) = invl;
+    // spare lanes: the junk slot (a two-slot one when wreal is wider than real)
+    wreal* const jk = reinterpret_cast<wreal*>(
+        &sh.junk[std::is_same<wreal, real>::value ? (lane & 63) : (lane & 62)]);
+    *(lane < 16 ? &sh.inv[lane] : jk) = invl;
     if (NT > 64) __syncthreads();
 #if MHPC_BWS_WAVEBAR == 1
     else __builtin_amdgcn_wave_barrier();
@@ -489,10 +504,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
 #pragma unroll
       for (int c = 0; c < 4; ++c) Qi[a * 4 + c] = (inv[a * 4 + c] + inv[c * 4 + a]) / 2;
     // dV += -Qu' inv Qu, unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
-    real s = 0;
+    wreal s = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      real t = 0;
+      wreal t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += qu(sh, QS, NX, k, QV) * inv[k * 4 + c];
       s += t * qu(sh, QS, NX, c, QV);
@@ -500,7 +515,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     // s and psd are uniform: every lane of wave 0 writes the same value (no divergent
     // branch); the other waves of a 128-thread block must not re-read the updated dV
     const real dv0 = sh.dV;
-    *(lane < 64 ? &sh.dV : &sh.junk[lane & 63]) = psd ? dv0 + -s : dv0;
+    *(lane < 64 ? &sh.dV : &sh.junk[lane & 63]) = psd ? real(dv0 + -s) : dv0;
   }
   {
     // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
@@ -509,20 +524,20 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     constexpr int NI = NX + 1, GC = NT / NI, T5 = (NX + 1 + GC - 1) / GC;
     const int i = lane % NI, g = lane / NI;
     const int si = i < NX ? i : QV;
-    real qi[4];
+    wreal qi[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) qi[k] = qu(sh, QS, NX, k, si);
-    real tq[4];
+    wreal tq[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      real t = 0;
+      wreal t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
       tq[c] = t;
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      *(g == 0 ? (i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) : &sh.junk[lane & 63]) = -tq[c];
+      *(g == 0 ? (i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) : &sh.junk[lane & 63]) = real(-tq[c]);
     constexpr int C = T5 < CH5 ? T5 : CH5;
 #pragma unroll
     for (int t0 = 0; t0 < T5; t0 += C) {
@@ -532,14 +547,14 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         if (t0 + u >= T5) continue;
         const int j = g + GC * (t0 + u);
         const int sj = j < NX ? j : QV;
-        real sacc = 0;
+        wreal sacc = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) sacc += tq[c] * qu(sh, QS, NX, c, sj);
         const real qij = sh.Q[i * QS + sj];
         const real qji = sh.Q[(j < NX ? j : 0) * QS + i];
         const real sym = (qij + qji) / 2;
         const real base = j < NX ? sym : qij;
-        acc[u] = base - sacc;
+        acc[u] = real(base - sacc);
       }
 #pragma unroll
       for (int u = 0; u < C; ++u) {

@@ -64,19 +64,18 @@ static __device__ __forceinline__ real log_pos(real x) {
 // The reference's pow() calls with integer exponents are evaluated exactly as products:
 // pow(t, 2) = t*t (the correctly rounded square), pow(t, 1) = t, pow(t, 0) = 1 (also for
 // NaN, as pow defines), pow(g, -2) = 1/(g*g) (within 1 ulp of the correctly rounded value).
+// Branch-free: one log per constraint (of g or of delta, whichever branch the lane takes)
+// instead of both sides of a divergent branch; each lane computes exactly the operations of
+// its branch.
 static __device__ __forceinline__ void reduced_barrier(real g, real delta, real* B, real* Bz,
                                                 real* Bzz) {
   MHPC_NO_FMA_F32
-  if (g > delta) {
-    *B = -log_pos(g);
-    *Bz = -1.0 / g;
-    *Bzz = 1.0 / (g * g);
-  } else {
-    const real t = (g - 2 * delta) / ((2 - 1) * delta);
-    *B = (real)(2 - 1) / 2 * (t * t - 1) - log_pos(delta);
-    *Bz = t / delta;
-    *Bzz = 1.0;
-  }
+  const bool in = g > delta;
+  const real lg = log_pos(in ? g : delta);
+  const real t = (g - 2 * delta) / ((2 - 1) * delta);
+  *B = in ? -lg : (real)(2 - 1) / 2 * (t * t - 1) - lg;
+  *Bz = in ? -1.0 / g : t / delta;
+  *Bzz = in ? 1.0 / (g * g) : real(1.0);
 }
 
 // Running cost value incl. the ReB barrier of WB phases (CostBase.cpp:4-16,

@@ -122,6 +122,17 @@ MHPC_HD void sin_cos(real a, real* s, real* c) {
   *s = sinf(a);
   *c = cosf(a);
 #endif
+#elif defined(__HIP_DEVICE_COMPILE__)
+  // the library path as a wave-uniform branch (taken only when some lane's argument is out
+  // of the short reduction's range): no exec-mask join in the knot loops
+  sin_cos_short(a, s, c);
+  if (__builtin_amdgcn_ballot_w64(!(fabs(a) <= 1e5))) {
+    real sl, cl;
+    sincos(a, &sl, &cl);
+    const bool big = !(fabs(a) <= 1e5);
+    *s = big ? sl : *s;
+    *c = big ? cl : *c;
+  }
 #else
   if (fabs(a) <= 1e5) {
     sin_cos_short(a, s, c);
@@ -133,6 +144,33 @@ MHPC_HD void sin_cos(real a, real* s, real* c) {
     *c = cos(a);
 #endif
   }
+#endif
+}
+// sin_cos of N angles at once: the short reductions and polynomials of all N side by side
+// (one set of constants, interleaved chains) and one wave-uniform library fallback for them
+// all; per angle the same value as sin_cos.
+template <int N>
+MHPC_HD void sin_cos_n(const real (&a)[N], real (&s)[N], real (&c)[N]) {
+#if !defined(MHPC_FP32) && defined(__HIP_DEVICE_COMPILE__)
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    sin_cos_short(a[i], &s[i], &c[i]);
+    big = big || !(fabs(a[i]) <= 1e5);
+  }
+  if (__builtin_amdgcn_ballot_w64(big)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      real sl, cl;
+      sincos(a[i], &sl, &cl);
+      const bool bi = !(fabs(a[i]) <= 1e5);
+      s[i] = bi ? sl : s[i];
+      c[i] = bi ? cl : c[i];
+    }
+  }
+#else
+#pragma unroll
+  for (int i = 0; i < N; ++i) sin_cos(a[i], &s[i], &c[i]);
 #endif
 }
 MHPC_HD void sin_cos(Dual a, Dual* s, Dual* c) {

@@ -59,6 +59,19 @@ __device__ __forceinline__ real fb_dot(const real* Kr, const real* x, const real
   return fb;
 }
 
+// Problems per block of the pair variant (at most 32 / n_cand = 3 with 10 candidates).
+#ifndef MHPC_RO_PAIR_PPB
+#define MHPC_RO_PAIR_PPB 3
+#endif
+constexpr int RO_PAIR_PPB = MHPC_RO_PAIR_PPB;
+
+// Ring depth of the pair variant's dynamics -> cost hand-over (2: a barrier per knot record;
+// 4: one per two records)
+#ifndef MHPC_RO_RING_PAIR
+#define MHPC_RO_RING_PAIR 4
+#endif
+constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
+
 // native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
 typedef real sreal2 __attribute__((ext_vector_type(2)));
 constexpr int ST_PPW = 6;      // problems per staged wave (64 lanes / 10 candidates)
@@ -174,8 +187,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
                                                              int max_ddp, int full) {
   MHPC_NO_FMA_F32
   const int nc = full ? 1 : sp.n_cand;
-  const int ppw = (PAIR ? 32 : 64) / nc;
-  constexpr int SNP = PAIR ? 3 : ST_PPW;  // staged problem slots (ppw <= SNP when staged)
+  const int ppw = PAIR ? min(32 / nc, RO_PAIR_PPB) : 64 / nc;
+  constexpr int SNP = PAIR ? RO_PAIR_PPB : ST_PPW;  // staged problem slots (ppw <= SNP when staged)
   const int t = threadIdx.x, lane = t & 63;
   const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
   const int cl = (PAIR && w0) ? (lane >> 1) : lane;
@@ -184,12 +197,16 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   const int b = blockIdx.x * ppw + lp;
   const bool in = lp < ppw && b < sp.B;
 
-  __shared__ real ring[PIPE ? 2 : 1][RING_W][64];
+  // ring of RD knot records; the waves meet at a barrier every RD / 2 records
+  constexpr int RD = PIPE ? (PAIR ? RO_RING_PAIR : 2) : 1;
+  constexpr int RG = PIPE ? RD / 2 : 1;  // records per barrier
+  static_assert(RG >= 1 && (RG & (RG - 1)) == 0, "ring depth");
+  __shared__ real ring[RD][RING_W][64];
   __shared__ real sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
   __shared__ int sAny;
   __shared__ int sNom[ST ? ST_PPW : 1];
-  __shared__ sreal2 stage2[ST ? ST_PPW * ST_PAIRS : 1];
-  __shared__ real sRef[ST ? ST_PPW : 1][ST ? ST_RMAX + 1 : 1];  // +1: distinct banks
+  __shared__ sreal2 stage2[ST ? SNP * ST_PAIRS : 1];
+  __shared__ real sRef[ST ? SNP : 1][ST ? ST_RMAX + 1 : 1];  // +1: distinct banks
 #ifdef MHPC_RO_TIMING
   unsigned long long ro_cyc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -272,8 +289,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
       else stage_issue<false, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
     }
+    int pend = -1;  // cost wave: knot record handed over but not consumed yet (RG > 1)
     for (int k = 0; k < N - 1; ++k, ++q) {
-      const int s = PIPE ? (q & 1) : 0;
+      const int s = PIPE ? (q & (RD - 1)) : 0;
+      // barrier after every RG-th record (the phase's terminal record always gets one)
+      const bool bar = (q & (RG - 1)) == RG - 1;
       real rr[RING_W];
       const int kc = k & (CH - 1);
       RO_T(tk0);
@@ -389,7 +409,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
             if (i < nrec) ring[s][i][lane] = rr[i];
         }
       }
-      if (PIPE) __syncthreads();
+      if (PIPE && bar) __syncthreads();
 #ifdef MHPC_RO_TIMING
       if (lane == 0 && w0 && run) {
         const unsigned long long tk3 = clock64();
@@ -402,18 +422,27 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         ro_cyc[9] += tkc - tk0;
       }
 #endif
-      if (w1 && run) {
+      // cost wave: the running cost of knot kk from ring slot sl (knot order: the serial
+      // rollout's association), and the knot's record store
+      auto consume = [&](int kk, int sl) {
         real r[RING_W];
 #pragma unroll
-        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[s][i][lane] : rr[i]) : real(0.0);
-        const real pos = sref ? sRef[lp][k] : refpos[k];
+        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[sl][i][lane] : rr[i]) : real(0.0);
+        const real pos = sref ? sRef[lp][kk] : refpos[kk];
         V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, delta, etq, egr)
                 : fb_running_cost(sp, mode, dt, pos, r, r + 6);
-        store_rec(r, nrec, ko + k);
+        store_rec(r, nrec, ko + kk);
+      };
+      if (w1 && run) {
+        if (bar) {
+          if (RG > 1 && pend >= 0) consume(pend, (s - 1) & (RD - 1));
+          consume(k, s);
+        }
       }
+      if (RG > 1) pend = bar ? -1 : k;  // RG = 2: at most one record waits
     }
     // terminal state of the phase, then the transition (wave 0)
-    const int s = PIPE ? (q & 1) : 0;
+    const int s = PIPE ? (q & (RD - 1)) : 0;
     ++q;
     real xe[RING_W];
     if (w0 && run) {
@@ -443,6 +472,16 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     if (PIPE) __syncthreads();
     if (w1) {
       if (run) {
+        if (RG > 1 && pend >= 0) {  // the last knot record of the phase, if still waiting
+          real r[RING_W];
+          const int kk = N - 2, sl = (s - 1) & (RD - 1);
+#pragma unroll
+          for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? ring[sl][i][lane] : real(0.0);
+          const real pos = sref ? sRef[lp][kk] : refpos[kk];
+          V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, delta, etq, egr)
+                  : fb_running_cost(sp, mode, dt, pos, r, r + 6);
+          store_rec(r, nrec, ko + kk);
+        }
         if (PIPE) {
 #pragma unroll
           for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? ring[s][i][lane] : real(0.0);
@@ -1315,7 +1354,7 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
 #endif
   bool st = ppw <= ST_PPW;
   // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
-  const int ppw2 = 32 / sp.n_cand;
+  const int ppw2 = std::min(32 / sp.n_cand, RO_PAIR_PPB);
   const int nblk2 = ppw2 > 0 ? (sp.B + ppw2 - 1) / ppw2 : 0;
 #ifdef MHPC_RO_PAIR_MAX_BLK
   const int pair_max = MHPC_RO_PAIR_MAX_BLK;

@@ -30,6 +30,7 @@
 // tests/test_pair_host.py) and a problem's result does not depend on which line-search
 // variant its batch size selects.
 #pragma once
+#include <type_traits>
 #include "mhpc_dual.h"
 
 // MHPC_WB_FMA (timing experiments only) lets the compiler contract the whole-body model
@@ -92,15 +93,31 @@ struct WbGeo {
 };
 
 // xq = q (7), xv = qdot (7)
-template <class Q, class V>
+// BATCH: the real-valued angles through sin_cos_n (fewer instructions; more live registers,
+// so the register-bound partials keep the one-at-a-time form).  Same values either way.
+template <class Q, class V, bool BATCH = true>
 MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g) {
-  sin_cos(xq[2], &g.sth, &g.cth);
+  if constexpr (BATCH && std::is_same<Q, real>::value) {
+    // the five link angles' sines / cosines side by side (sin_cos_n)
+    const real a[5] = {xq[2], xq[2] + xq[3], (xq[2] + xq[3]) + xq[4], xq[2] + xq[5],
+                       (xq[2] + xq[5]) + xq[6]};
+    real sv[5], cv[5];
+    sin_cos_n<5>(a, sv, cv);
+    g.sth = sv[0]; g.cth = cv[0];
+    g.leg[0].s1 = sv[1]; g.leg[0].c1 = cv[1]; g.leg[0].s2 = sv[2]; g.leg[0].c2 = cv[2];
+    g.leg[1].s1 = sv[3]; g.leg[1].c1 = cv[3]; g.leg[1].s2 = sv[4]; g.leg[1].c2 = cv[4];
+  } else {
+    sin_cos(xq[2], &g.sth, &g.cth);
+    for (int f = 0; f < 2; ++f) {
+      const int ih = 3 + 2 * f, ik = 4 + 2 * f;
+      const Q a1 = xq[2] + xq[ih];
+      const Q a2 = a1 + xq[ik];
+      sin_cos(a1, &g.leg[f].s1, &g.leg[f].c1);
+      sin_cos(a2, &g.leg[f].s2, &g.leg[f].c2);
+    }
+  }
   for (int f = 0; f < 2; ++f) {
     const int ih = 3 + 2 * f, ik = 4 + 2 * f;
-    const Q a1 = xq[2] + xq[ih];
-    const Q a2 = a1 + xq[ik];
-    sin_cos(a1, &g.leg[f].s1, &g.leg[f].c1);
-    sin_cos(a2, &g.leg[f].s2, &g.leg[f].c2);
     g.leg[f].w1 = xv[2] + xv[ih];
     g.leg[f].w2 = g.leg[f].w1 + xv[ik];
   }
@@ -419,7 +436,7 @@ struct WbKnot {
 template <int SF>
 MHPC_HD void wb_knot_primal(const real* x, const real* u, WbKnot& K) {
   MHPC_NO_FMA_WB
-  wb_geometry<real, real>(x, x + 7, K.g);
+  wb_geometry<real, real, false>(x, x + 7, K.g);
   real h[7], v[7];
   wb_mass_bias<real, real>(x + 7, K.g, K.M, h);
   arrow_factor(K.M, K.AF);

@@ -172,15 +172,16 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   MHPC_NO_FMA_WB
   const real sg = back ? -real(1.0) : real(1.0);
   // geometry: the body pitch and the own leg's two links
-  real sth, cth;
-  sin_cos(x[2], &sth, &cth);
   const real qh = back ? x[5] : x[3], qk = back ? x[6] : x[4];
   const real qhd = back ? x[12] : x[10], qkd = back ? x[13] : x[11];
   LegGeo<real, real> L;
   const real a1 = x[2] + qh;
   const real a2 = a1 + qk;
-  sin_cos(a1, &L.s1, &L.c1);
-  sin_cos(a2, &L.s2, &L.c2);
+  real sv[3], cv[3];
+  sin_cos_n<3>({x[2], a1, a2}, sv, cv);
+  const real sth = sv[0], cth = cv[0];
+  L.s1 = sv[1]; L.c1 = cv[1];
+  L.s2 = sv[2]; L.c2 = cv[2];
   L.w1 = x[9] + qhd;
   L.w2 = L.w1 + qkd;
   PairLegMH lm;
