@@ -77,8 +77,13 @@ template <int NX> struct QShape {
 
 // Arithmetic type of the 4x4 control block of a knot (adjugate, determinant, Quu^-1, the
 // gains tq = Qux' Quu^-1 and the products that update H / G / dV with them): the solve's
-// type, or double in an fp32 build with MHPC_BWS_WIDE (the fp32 sweep's gains then carry the
-// rounding of the fp32 Q blocks only, not of an fp32 inversion).
+// type, or double in the fp32 build (MHPC_BWS_WIDE, default; whole-body knots only): the fp32
+// sweep's gains then carry the rounding of the fp32 Q blocks only, not of an fp32 inversion
+// (C5 fp32: worst cost error vs the fp64 oracle 5.4e-3 -> 4.0e-3, gains after one sweep 3x
+// closer in the stance phases).
+#ifndef MHPC_BWS_WIDE
+#define MHPC_BWS_WIDE 1
+#endif
 #if defined(MHPC_FP32) && MHPC_BWS_WIDE
 using wreal = double;
 #else
@@ -112,7 +117,7 @@ struct BwsLds {
   alignas(16) real dust[4];
   real hx[14], Hs[9], G2v[14];
   alignas(16) real junk[64];  // write target of the spare lanes of a round (never read)
-  real dV;
+  acc dV;
   int fail;
 #ifdef MHPC_BWS_TIMING
   unsigned long long cyc[12], tlast;
@@ -323,6 +328,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
                              R45X&& r45x) {
   constexpr int NX = 2 * NQ, NR = NX + 4;
   constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
+  // the control block's arithmetic type: wreal for the whole-body knots (the fp32 sweep's
+  // gain errors come from them: tools/diag_fp32_stages.py), the solve's type for SRB knots
+  using wk = typename std::conditional<NQ == 7, wreal, real>::type;
   // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly, G taken as column NX
   // of [H | G].  Lane = (column j, row group g): the column stays in registers and the lane
   // runs T2 independent row chains.
@@ -428,10 +436,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
   // spread over lanes 0..15 (one 3x3 minor each) and broadcast back with readlane (no LDS
   // round trip); then, in the same round, tq = Qux' Quu_inv, K = -tq', du, dV and
   // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
-  wreal q0[4];
+  wk q0[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) q0[c] = qu(sh, QS, NX, 0, NX + c);
-  wreal adj = wreal(0.0);
+  wk adj = wk(0.0);
   bool psd;
   {
     // the PSD verdict is applied at the end of the round: a failed knot abandons the sweep
@@ -440,9 +448,9 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
     const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
 #define QM(r, c) qu(sh, QS, NX, r, NX + (c))
-    const wreal m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
-    const wreal m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
-    const wreal m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
+    const wk m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
+    const wk m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
+    const wk m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
 #undef QM
     real A[16];
 #pragma unroll
@@ -458,16 +466,16 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     psd = ldlt_is_positive4(A);
 #endif
     // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
-    const wreal det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
+    const wk det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
                          m02 * (m10 * m21 - m11 * m20);
     adj = ((i + j) & 1) ? -det3 : det3;
   }
-  const wreal det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
+  const wk det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
                       q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
-  const wreal invl = adj / det;
-  wreal Qi[16];
+  const wk invl = adj / det;
+  wk Qi[16];
   {
-    wreal inv[16];  // unsymmetrised inverse (uniform)
+    wk inv[16];  // unsymmetrised inverse (uniform)
 #if MHPC_BWS_INVLDS
     // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
     // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
@@ -480,10 +488,10 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
 #ifndef MHPC_BWS_WAVEBAR
 #define MHPC_BWS_WAVEBAR 0
 #endif
-    // spare lanes: the junk slot (a two-slot one when wreal is wider than real)
+    // spare lanes: the junk slot (a two-slot one when wk is wider than real)
     wreal* const jk = reinterpret_cast<wreal*>(
         &sh.junk[std::is_same<wreal, real>::value ? (lane & 63) : (lane & 62)]);
-    *(lane < 16 ? &sh.inv[lane] : jk) = invl;
+    *(lane < 16 ? &sh.inv[lane] : jk) = wreal(invl);
     if (NT > 64) __syncthreads();
 #if MHPC_BWS_WAVEBAR == 1
     else __builtin_amdgcn_wave_barrier();
@@ -504,18 +512,20 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
 #pragma unroll
       for (int c = 0; c < 4; ++c) Qi[a * 4 + c] = (inv[a * 4 + c] + inv[c * 4 + a]) / 2;
     // dV += -Qu' inv Qu, unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
-    wreal s = 0;
+    wk s = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      wreal t = 0;
+      wk t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += qu(sh, QS, NX, k, QV) * inv[k * 4 + c];
       s += t * qu(sh, QS, NX, c, QV);
     }
     // s and psd are uniform: every lane of wave 0 writes the same value (no divergent
     // branch); the other waves of a 128-thread block must not re-read the updated dV
-    const real dv0 = sh.dV;
-    *(lane < 64 ? &sh.dV : &sh.junk[lane & 63]) = psd ? real(dv0 + -s) : dv0;
+    const acc dv0 = sh.dV;
+    acc* const jd = reinterpret_cast<acc*>(
+        &sh.junk[std::is_same<acc, real>::value ? (lane & 63) : (lane & 62)]);
+    *(lane < 64 ? &sh.dV : jd) = psd ? acc(dv0 + -s) : dv0;
   }
   {
     // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
@@ -524,13 +534,13 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     constexpr int NI = NX + 1, GC = NT / NI, T5 = (NX + 1 + GC - 1) / GC;
     const int i = lane % NI, g = lane / NI;
     const int si = i < NX ? i : QV;
-    wreal qi[4];
+    wk qi[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) qi[k] = qu(sh, QS, NX, k, si);
-    wreal tq[4];
+    wk tq[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      wreal t = 0;
+      wk t = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
       tq[c] = t;
@@ -547,7 +557,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         if (t0 + u >= T5) continue;
         const int j = g + GC * (t0 + u);
         const int sj = j < NX ? j : QV;
-        wreal sacc = 0;
+        wk sacc = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) sacc += tq[c] * qu(sh, QS, NX, c, sj);
         const real qij = sh.Q[i * QS + sj];

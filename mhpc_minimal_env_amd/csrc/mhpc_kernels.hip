@@ -202,7 +202,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   constexpr int RG = PIPE ? RD / 2 : 1;  // records per barrier
   static_assert(RG >= 1 && (RG & (RG - 1)) == 0, "ring depth");
   __shared__ real ring[RD][RING_W][64];
-  __shared__ real sJ[64], sViol[64], sV[MAXP][64], sH[MAXP][64];
+  __shared__ acc sJ[64], sViol[64], sV[MAXP][64];
+  __shared__ real sH[MAXP][64];
   __shared__ int sAny;
   __shared__ int sNom[ST ? ST_PPW : 1];
   __shared__ sreal2 stage2[ST ? SNP * ST_PAIRS : 1];
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const real* x0 = d.x0 + (size_t)b * 14;
     for (int i = 0; i < 14; ++i) x[i] = x0[i];
   }
-  real J = 0, viol2 = 0;
+  acc J = 0, viol2 = 0;
   int q = 0;  // ring records handed over so far
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
@@ -260,7 +261,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
     const int nx = wb ? 14 : 6, nrec = wb ? RING_W : 14;
-    real V = 0, delta = 0, etq = 0, egr = 0;
+    acc V = 0;
+    real delta = 0, etq = 0, egr = 0;
     if (w1 && run && wb) { delta = st->delta[p]; etq = st->eps_tq[p]; egr = st->eps_grf[p]; }
     real f[4], sc[2];
     if (w0 && run && !wb) {
@@ -490,14 +492,14 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         if (wb) {
           real rx[14];
           wb_term_ref(sp, mode, refT, rx);
-          real Phi = 0;
+          acc Phi = 0;
           for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
-          Phi = Phi * real(0.5);
+          Phi = Phi * acc(0.5);
           if (ntc_of(mode, true)) {
             h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
             if (sp.AL_active) {
-              const real sg = st->sigma[p], lam = st->lambda[p];
-              const real sh2 = sg * h / 2;
+              const acc sg = st->sigma[p], lam = st->lambda[p];
+              const acc sh2 = sg * h / 2;
               Phi += 50 * (sh2 * sh2 + lam * h);
             }
           }
@@ -505,12 +507,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         } else {
           real rx[6];
           fb_term_ref(sp, refT, rx);
-          real Phi = 0;
+          acc Phi = 0;
           for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
-          V += Phi * real(0.5);
+          V += Phi * acc(0.5);
         }
         J += V;
-        viol2 += h * h;
+        viol2 += acc(h) * h;
         sV[p][lane] = V;
         sH[p][lane] = h;
         store_rec(xe, nx, ko + N - 1);
@@ -546,11 +548,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     return;
   }
   if (w1 && run && j == 0) {
-    const real cost_prev = st->J;
+    const acc cost_prev = st->J;
     int sel = nc - 1, nls = nc + 1;
     for (int c = 0; c < nc; ++c) {
       const real e = sp.eps[c];
-      const real rhs = cost_prev + sp.gamma * e * (1 - e / 2) * st->dV_exp;
+      const acc rhs = cost_prev + sp.gamma * e * (1 - e / 2) * st->dV_exp;
       if (sJ[lane + c] <= rhs) { sel = c; nls = c + 1; break; }
     }
     const int sl = lane + sel;
@@ -601,12 +603,13 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
   real x[14];
   const real* x0 = d.x0 + (size_t)b * 14;
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
-  real J = 0, viol2 = 0;
+  acc J = 0, viol2 = 0;
   for (int p = 0; p < sp.P; ++p) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
     const real dt = sp.dt[p];
     const real* refpos = d.refpos + (size_t)b * sp.NK + ko;
-    real V = 0, h = 0;
+    acc V = 0;
+    real h = 0;
     if (p < sp.n_wb) {
       const real delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
       for (int k = 0; k < N - 1; ++k) {
@@ -627,14 +630,14 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
       }
       real rx[14];
       wb_term_ref(sp, mode, refpos[N - 1], rx);
-      real Phi = 0;
+      acc Phi = 0;
       for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.wQf[mode - 1][i] * ee; }
-      Phi = Phi * real(0.5);
+      Phi = Phi * acc(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
         if (sp.AL_active) {
-          const real sg = st->sigma[p], lam = st->lambda[p];
-          const real sh2 = sg * h / 2;
+          const acc sg = st->sigma[p], lam = st->lambda[p];
+          const acc sh2 = sg * h / 2;
           Phi += 50 * (sh2 * sh2 + lam * h);
         }
       }
@@ -672,15 +675,15 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
       }
       real rx[6];
       fb_term_ref(sp, refpos[N - 1], rx);
-      real Phi = 0;
+      acc Phi = 0;
       for (int i = 0; i < 6; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.fQf[mode - 1][i] * ee; }
-      V += Phi * real(0.5);
+      V += Phi * acc(0.5);
     }
     J += V;
-    viol2 += h * h;
+    viol2 += acc(h) * h;
   }
-  Jo[t] = J;
-  vo[t] = sqrt(viol2);
+  Jo[t] = real(J);
+  vo[t] = real(sqrt(viol2));
 }
 
 // ============================================================================================
@@ -1103,7 +1106,8 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   if (!st->active) return;
   const int lane = threadIdx.x;
   __shared__ real sc[MHPC_MAX_KNOTS];
-  __shared__ real sV[MAXP], sH[MAXP];
+  __shared__ acc sV[MAXP];
+  __shared__ real sH[MAXP];
   const bool reb_off = (st->viol > real(0.05)) || al_iter == 1;
   // solve() captures _option.ReB_active at its start, restores it every AL iteration
   const int cap_reb = al_iter == 1 ? st->opt_reb : st->cap_reb;
@@ -1128,20 +1132,21 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   __syncthreads();
   if (lane < sp.P) {
     const int p = lane, mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    real V = 0, h = 0;
+    acc V = 0;
+    real h = 0;
     for (int k = 0; k < N - 1; ++k) V += sc[ko + k];
     const real* x = traj_ptr(sp, d, b, nom, ko + N - 1);
     if (p < sp.n_wb) {
       real rx[14];
       wb_term_ref(sp, mode, refpos[ko + N - 1], rx);
-      real Phi = 0;
+      acc Phi = 0;
       for (int i = 0; i < 14; ++i) { const real e = x[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
-      Phi = Phi * real(0.5);
+      Phi = Phi * acc(0.5);
       if (ntc_of(mode, true)) {
         h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
         if (sp.AL_active) {
-          const real s = st->sigma[p], lam = st->lambda[p];
-          const real sh2 = s * h / 2;
+          const acc s = st->sigma[p], lam = st->lambda[p];
+          const acc sh2 = s * h / 2;
           Phi += 50 * (sh2 * sh2 + lam * h);
         }
       }
@@ -1149,19 +1154,19 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
     } else {
       real rx[6];
       fb_term_ref(sp, refpos[ko + N - 1], rx);
-      real Phi = 0;
+      acc Phi = 0;
       for (int i = 0; i < 6; ++i) { const real e = x[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
-      V += Phi * real(0.5);
+      V += Phi * acc(0.5);
     }
     sV[p] = V;
     sH[p] = h;
   }
   __syncthreads();
   if (lane == 0) {
-    real J = 0, viol2 = 0;
+    acc J = 0, viol2 = 0;
     for (int p = 0; p < sp.P; ++p) {
       J += sV[p];
-      viol2 += sH[p] * sH[p];
+      viol2 += acc(sH[p]) * sH[p];
       st->V[p] = sV[p];
       st->h[p] = sH[p];
     }

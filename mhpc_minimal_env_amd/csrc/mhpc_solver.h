@@ -75,9 +75,17 @@ struct SolveParams {
   CostParams cw;
 };
 
+// Costs, their sums and the expected cost change are accumulated and compared in fp64 in
+// both builds (the fp32 build keeps its dynamics, partials and sweep in fp32): a total cost
+// of ~1e5 summed over ~700 knots in fp32 carries errors of the size of the Armijo margins.
+using acc = double;
+
 struct ProbState {
-  real J, viol, dV_exp, reg, cost_prev;
-  real V[MAXP], dV[MAXP], h[MAXP];
+  acc J, viol, dV_exp;
+  real reg;
+  acc cost_prev;
+  acc V[MAXP], dV[MAXP];
+  real h[MAXP];
   real sigma[MAXP], lambda[MAXP], delta[MAXP], eps_tq[MAXP], eps_grf[MAXP];
   int32_t status;      // mhpc_solve_status
   int32_t active;      // still inside the AL loop

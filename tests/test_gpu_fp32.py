@@ -8,14 +8,16 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# Measured on MI355X (64 problems; fp32 sweep contracted without the SLP vectoriser,
-# mhpc_minimal_env_amd/csrc/Makefile): trace identical for 64/64, relative cost error median
-# 3.4e-5, max 6.2e-3; the 64-problem sample of the batch-4096 test (test_gpu_variants.py):
-# traces 63/64, max 1.0e-2.  The worst problems' error sits in one WB phase's value (the
-# touchdown AL term amplifies fp32 round-off over the AL x DDP iterations).
-FP32_TRACE_MIN = 0.9      # problems that take the fp64 decisions
-FP32_J_TOL = 2e-2         # relative cost error of those problems, worst case
-FP32_J_MEDIAN_TOL = 1e-4  # ... and typical
+# Measured on MI355X (round 3): 64 problems -- traces identical 64/64, relative cost error
+# median 1.4e-5, max 1.8e-3; the batch-4103 sample of test_gpu_variants.py -- traces 63/63
+# (distinct indices), max 1.4e-3.  The fp32 build sums costs and compares the Armijo
+# condition in fp64 (mhpc_solver.h `acc`) and inverts the whole-body knots' 4x4 control block
+# in fp64 (mhpc_bws.hip, MHPC_BWS_WIDE): the gains of one fp32 sweep were 1e-2 off in the
+# stance phases (tools/diag_fp32_stages.py), the source of the earlier 5e-3..1e-2 cost errors;
+# fp64 cost accumulation alone left them unchanged.
+FP32_TRACE_MIN = 1.0      # problems that take the fp64 decisions
+FP32_J_TOL = 5e-3         # relative cost error of those problems, worst case
+FP32_J_MEDIAN_TOL = 5e-5  # ... and typical
 
 
 def test_c5_fp32_vs_fp64_oracle(need_gpu):
