@@ -71,6 +71,9 @@ constexpr int RO_PAIR_PPB = MHPC_RO_PAIR_PPB;
 #define MHPC_RO_RING_PAIR 4
 #endif
 constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
+#ifndef MHPC_RO_PREFETCH
+#define MHPC_RO_PREFETCH 1
+#endif
 
 // native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
 typedef real sreal2 __attribute__((ext_vector_type(2)));
@@ -189,6 +192,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   const int nc = full ? 1 : sp.n_cand;
   const int ppw = PAIR ? min(32 / nc, RO_PAIR_PPB) : 64 / nc;
   constexpr int SNP = PAIR ? RO_PAIR_PPB : ST_PPW;  // staged problem slots (ppw <= SNP when staged)
+  constexpr bool PF = PAIR && ST && MHPC_RO_PREFETCH;  // register prefetch of the next knot
   const int t = threadIdx.x, lane = t & 63;
   const bool w0 = PIPE ? (t >> 6) == 0 : true, w1 = PIPE ? (t >> 6) == 1 : true;
   const int cl = (PAIR && w0) ? (lane >> 1) : lane;
@@ -247,7 +251,6 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     for (int i = 0; i < 14; ++i) x[i] = x0[i];
   }
   acc J = 0, viol2 = 0;
-  int q = 0;  // ring records handed over so far
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
   auto store_rec = [&](const real* r, int n, int kk) {
@@ -256,266 +259,391 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     for (int i = 0; i < RING_W / 2; ++i)
       if (2 * i < n) o[i] = real2{r[2 * i], r[2 * i + 1]};
   };
-  for (int p = 0; p < sp.P; ++p) {
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
-    const bool wb = p < sp.n_wb;
-    const int nx = wb ? 14 : 6, nrec = wb ? RING_W : 14;
-    acc V = 0;
-    real delta = 0, etq = 0, egr = 0;
-    if (w1 && run && wb) { delta = st->delta[p]; etq = st->eps_tq[p]; egr = st->eps_grf[p]; }
-    real f[4], sc[2];
-    if (w0 && run && !wb) {
-      plan_foothold(x, dt * N, mode, f);
-      srb_contact(mode, sc);
-    }
-    const real* refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
-    const int b0 = blockIdx.x * ppw;
-    // position references of the phase: staged in LDS by the cost wave (one round trip per
-    // phase), read from HBM per knot when the phase is longer than the stage
-    const bool sref = ST && N <= ST_RMAX;
-    if (sref && w1) {
-#pragma unroll
-      for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
-        const int f = lane + 64 * i, rl = f / ST_RMAX, rk = f - rl * ST_RMAX;
-        if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
-      }
-    }
-    const real refT = (w1 && run) ? (sref ? sRef[lp][N - 1] : refpos[N - 1]) : real(0.0);
-    const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+  const int b0 = blockIdx.x * ppw;
+  real f[4] = {0, 0, 0, 0}, sc[2] = {0, 0};  // SRB phase: foothold, contact flags
+  sreal2 pf[ST_PPW * 3];                    // the next chunk's stage loads in flight
+  // PF (pair variant): the feedback operands of knot k+1 (own K rows, nominal x / u, du) are
+  // read from the stage into registers at the end of knot k, so their LDS latency overlaps
+  // the hand-over instead of heading the next knot's dependent chain; the next chunk is
+  // dropped into the stage right after the last knot of a chunk has read it.
+  real pK[28], pX[14], pU[4], pD[4];
+  auto prefetch = [&](bool wb, int kk) {
+    const int kcc = kk & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
     const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
     const int D0 = wb ? Stage<true>::D0 : Stage<false>::D0;
-    const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
-    sreal2 pf[ST_PPW * 3];
-    if (ST && w0) {
+    const real* sgp = reinterpret_cast<const real*>(stage2 + lp * ST_PAIRS);
+    const real* nk = sgp + 2 * (Stage<true>::T0 + kcc * TP);
+    const real* Kk = sgp + 2 * kcc * KP;
+    const real* duk = sgp + 2 * (D0 + 2 * kcc);
+    if (wb) {
+      const int r0 = back ? 2 : 0;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+#pragma unroll
+        for (int c = 0; c < 14; ++c) pK[ii * 14 + c] = Kk[(r0 + ii) * 14 + c];
+        pU[ii] = nk[14 + r0 + ii];
+        pD[ii] = duk[r0 + ii];
+      }
+#pragma unroll
+      for (int c = 0; c < 14; ++c) pX[c] = nk[c];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 24; ++i) pK[i] = Kk[i];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) pX[c] = nk[c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { pU[i] = nk[6 + i]; pD[i] = duk[i]; }
+    }
+  };
+  // drop the loaded chunk (knots k1..) into the stage and fetch the next one (all lanes of
+  // the dynamics wave: the loads are cooperative)
+  auto chunk_turn = [&](bool wb, int ko, int N, int k1) {
+    const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+    stage_drop<SNP>(lane, pf, stage2);
+    if (k1 + CH < N - 1) {
+      const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
+      if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, k1 + CH, N - 1, nomv, pf);
+      else stage_issue<false, SNP>(sp, d, SL, b0, ko, k1 + CH, N - 1, nomv, pf);
+    }
+  };
+  // dynamics side, phase start: SRB foothold / contact, first chunk of the stage
+  auto dyn_phase_begin = [&](int p) {
+    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const bool wb = p < sp.n_wb;
+    if (run && !wb) {
+      plan_foothold(x, sp.dt[p] * N, mode, f);
+      srb_contact(mode, sc);
+    }
+    if (ST) {
+      const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
       if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
       else stage_issue<false, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
     }
-    int pend = -1;  // cost wave: knot record handed over but not consumed yet (RG > 1)
-    for (int k = 0; k < N - 1; ++k, ++q) {
-      const int s = PIPE ? (q & (RD - 1)) : 0;
-      // barrier after every RG-th record (the phase's terminal record always gets one)
-      const bool bar = (q & (RG - 1)) == RG - 1;
-      real rr[RING_W];
-      const int kc = k & (CH - 1);
-      RO_T(tk0);
-      if (ST && w0 && kc == 0) {  // chunk boundary: drop the loaded chunk, fetch the next
-        stage_drop<SNP>(lane, pf, stage2);
-#ifdef MHPC_RO_TIMING
-        if (lane == 0) { const unsigned long long tdr = clock64(); ro_cyc[10] += tdr - tk0; }
-#endif
-        if (k + CH < N - 1) {
-          if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
-          else stage_issue<false, SNP>(sp, d, SL, b0, ko, k + CH, N - 1, nomv, pf);
-        }
-      }
-#ifdef MHPC_RO_TIMING
-      unsigned long long tk1 = 0, tk2 = 0;
-      const unsigned long long tkc = (lane == 0 && w0) ? clock64() : 0ull;
-#endif
-      if (w0 && run) {
-        const real* sgp = reinterpret_cast<const real*>(stage2 + lp * ST_PAIRS);
-        const real* nk = ST ? sgp + 2 * (Stage<true>::T0 + kc * TP) : traj_ptr(sp, d, b, nom, ko + k);
-        const real* Kk = ST ? sgp + 2 * kc * KP : d.K + ((size_t)b * sp.NK + ko + k) * 56;
-        const real* duk = ST ? sgp + 2 * (D0 + 2 * kc) : d.du + ((size_t)b * sp.NK + ko + k) * 4;
-        if (wb && PAIR) {
-          // the own leg's two torques (rows 2 back, 2 back + 1 of K)
-          real u2[2];
-          const int r0 = back ? 2 : 0;
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii) {
-            const real fb = fb_dot<14>(Kk + (r0 + ii) * 14, x, nk);
-            u2[ii] = (nk[14 + r0 + ii] + eps * duk[r0 + ii]) + fb;
-          }
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk1 = clock64();
-#endif
-          real xd[14], y[4];
-          wb_dynamics_pair(x, u2, mode, back, xd, y);
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk2 = clock64() + 0 * xd[13];
-#endif
-          // ring record split over the pair: x[7 back .. 7 back + 6], own u, own-slot y
-#pragma unroll
-          for (int i = 0; i < 7; ++i) rr[i] = back ? x[7 + i] : x[i];
-          rr[7] = u2[0]; rr[8] = u2[1];
-          rr[9] = back ? y[2] : y[0];
-          rr[10] = back ? y[3] : y[1];
-#pragma unroll
-          for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
-        } else if (wb) {
-          real u[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const real fb = fb_dot<14>(Kk + i * 14, x, nk);
-            u[i] = (nk[14 + i] + eps * duk[i]) + fb;
-          }
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk1 = clock64();
-#endif
-          real xd[14], y[4];
-          wb_dynamics<real>(x, u, mode, xd, y);
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk2 = clock64() + 0 * xd[13];
-#endif
-#pragma unroll
-          for (int i = 0; i < 14; ++i) rr[i] = x[i];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) { rr[14 + i] = u[i]; rr[18 + i] = y[i]; }
-#pragma unroll
-          for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
-        } else {
-          real u[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const real fb = fb_dot<6>(Kk + i * 6, x, nk);
-            u[i] = (nk[6 + i] + eps * duk[i]) + fb;
-          }
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk1 = clock64() + 0 * u[3];
-#endif
-          real xd[6];
-          srb_dynamics(x, u, f, sc, xd);
-#ifdef MHPC_RO_TIMING
-          if (lane == 0) tk2 = clock64() + 0 * xd[5];
-#endif
-#pragma unroll
-          for (int i = 0; i < 6; ++i) rr[i] = x[i];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = real(0.0); }
-          if (PAIR) {  // the pair splits the 14 record entries: 0..6 even lane, 7..13 odd
-#pragma unroll
-            for (int i = 0; i < 7; ++i) rr[i] = back ? rr[7 + i] : rr[i];
-          }
-#pragma unroll
-          for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
-        }
-      }
-      if (PIPE && w0 && run) {
-        if (PAIR) {
-          // WB: x half (7), u pair (2), y pair (2); SRB: half of the 14 entries
-          if (wb) {
-#pragma unroll
-            for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
-            ring[s][back ? 16 : 14][cl] = rr[7];
-            ring[s][back ? 17 : 15][cl] = rr[8];
-            ring[s][back ? 20 : 18][cl] = rr[9];
-            ring[s][back ? 21 : 19][cl] = rr[10];
-          } else {
-#pragma unroll
-            for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < RING_W; ++i)
-            if (i < nrec) ring[s][i][lane] = rr[i];
-        }
-      }
-      if (PIPE && bar) __syncthreads();
-#ifdef MHPC_RO_TIMING
-      if (lane == 0 && w0 && run) {
-        const unsigned long long tk3 = clock64();
-        if (wb) {
-          ro_cyc[0] += tk1 - tk0; ro_cyc[1] += tk2 - tk1; ro_cyc[2] += tk3 - tk2; ro_cyc[4]++;
-        } else {
-          ro_cyc[3] += tk3 - tk0; ro_cyc[5]++;
-          ro_cyc[6] += tk1 - tk0; ro_cyc[7] += tk2 - tk1; ro_cyc[8] += tk3 - tk2;
-        }
-        ro_cyc[9] += tkc - tk0;
-      }
-#endif
-      // cost wave: the running cost of knot kk from ring slot sl (knot order: the serial
-      // rollout's association), and the knot's record store
-      auto consume = [&](int kk, int sl) {
-        real r[RING_W];
-#pragma unroll
-        for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? (PIPE ? ring[sl][i][lane] : rr[i]) : real(0.0);
-        const real pos = sref ? sRef[lp][kk] : refpos[kk];
-        V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, delta, etq, egr)
-                : fb_running_cost(sp, mode, dt, pos, r, r + 6);
-        store_rec(r, nrec, ko + kk);
-      };
-      if (w1 && run) {
-        if (bar) {
-          if (RG > 1 && pend >= 0) consume(pend, (s - 1) & (RD - 1));
-          consume(k, s);
-        }
-      }
-      if (RG > 1) pend = bar ? -1 : k;  // RG = 2: at most one record waits
+    if (PF) {
+      chunk_turn(wb, ko, N, 0);
+      if (run) prefetch(wb, 0);
     }
-    // terminal state of the phase, then the transition (wave 0)
-    const int s = PIPE ? (q & (RD - 1)) : 0;
-    ++q;
-    real xe[RING_W];
-    if (w0 && run) {
+  };
+  // dynamics side, knot k of phase p: u = (u_nom + eps du) + K (x - x_nom), x+ = x + dt f(x, u);
+  // rr = the knot's record (x, u, y) as the ring / the cost side takes it
+  auto dyn_knot = [&](int p, int k, real* rr) {
+    const int mode = sp.mode[p], ko = sp.ko[p];
+    const real dt = sp.dt[p];
+    const bool wb = p < sp.n_wb;
+    const int kc = k & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
+    const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
+    const int D0 = wb ? Stage<true>::D0 : Stage<false>::D0;
+    const real* sgp = reinterpret_cast<const real*>(stage2 + lp * ST_PAIRS);
+    const real* nk = ST ? sgp + 2 * (Stage<true>::T0 + kc * TP) : traj_ptr(sp, d, b, nom, ko + k);
+    const real* Kk = ST ? sgp + 2 * kc * KP : d.K + ((size_t)b * sp.NK + ko + k) * 56;
+    const real* duk = ST ? sgp + 2 * (D0 + 2 * kc) : d.du + ((size_t)b * sp.NK + ko + k) * 4;
+    if (wb && PAIR) {
+      // the own leg's two torques (rows 2 back, 2 back + 1 of K)
+      real u2[2];
+      if (PF) {
 #pragma unroll
-      for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? x[i] : real(0.0);
-      if (PIPE && PAIR) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          const int e = (back ? 7 : 0) + i;
-          if (e < nx) ring[s][e][cl] = back ? x[7 + i] : x[i];
+        for (int ii = 0; ii < 2; ++ii) {
+          const real fb = fb_dot<14>(pK + ii * 14, x, pX);
+          u2[ii] = (pU[ii] + eps * pD[ii]) + fb;
         }
-      } else if (PIPE) {
-        for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
+      } else {
+        const int r0 = back ? 2 : 0;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const real fb = fb_dot<14>(Kk + (r0 + ii) * 14, x, nk);
+          u2[ii] = (nk[14 + r0 + ii] + eps * duk[r0 + ii]) + fb;
+        }
       }
-      if (wb && p + 1 < sp.P) {
-        if (mode == 2 || mode == 4) {
-          real xp[14], lam[2];
-          wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
-          for (int i = 0; i < 14; ++i) x[i] = xp[i];
-        }
-        if (p + 1 >= sp.n_wb) {
-          const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
-          x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
-        }
+      real xd[14], y[4];
+      wb_dynamics_pair(x, u2, mode, back, xd, y);
+      // ring record split over the pair: x[7 back .. 7 back + 6], own u, own-slot y
+#pragma unroll
+      for (int i = 0; i < 7; ++i) rr[i] = back ? x[7 + i] : x[i];
+      rr[7] = u2[0]; rr[8] = u2[1];
+      rr[9] = back ? y[2] : y[0];
+      rr[10] = back ? y[3] : y[1];
+#pragma unroll
+      for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
+    } else if (wb) {
+      real u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const real fb = fb_dot<14>(Kk + i * 14, x, nk);
+        u[i] = (nk[14 + i] + eps * duk[i]) + fb;
+      }
+      real xd[14], y[4];
+      wb_dynamics<real>(x, u, mode, xd, y);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) rr[i] = x[i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { rr[14 + i] = u[i]; rr[18 + i] = y[i]; }
+#pragma unroll
+      for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
+    } else {
+      real u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const real fb = PF ? fb_dot<6>(pK + i * 6, x, pX) : fb_dot<6>(Kk + i * 6, x, nk);
+        u[i] = PF ? (pU[i] + eps * pD[i]) + fb : (nk[6 + i] + eps * duk[i]) + fb;
+      }
+      real xd[6];
+      srb_dynamics(x, u, f, sc, xd);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) rr[i] = x[i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = real(0.0); }
+      if (PAIR) {  // the pair splits the 14 record entries: 0..6 even lane, 7..13 odd
+#pragma unroll
+        for (int i = 0; i < 7; ++i) rr[i] = back ? rr[7 + i] : rr[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) x[i] = x[i] + xd[i] * dt;
+    }
+  };
+  // phase transition after the phase's terminal state (MultiPhaseDDP.cpp:351-379)
+  auto transition = [&](int p) {
+    const int mode = sp.mode[p];
+    if (p < sp.n_wb && p + 1 < sp.P) {
+      if (mode == 2 || mode == 4) {
+        real xp[14], lam[2];
+        wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
+        for (int i = 0; i < 14; ++i) x[i] = xp[i];
+      }
+      if (p + 1 >= sp.n_wb) {
+        const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
+        x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
       }
     }
-    if (PIPE) __syncthreads();
-    if (w1) {
-      if (run) {
-        if (RG > 1 && pend >= 0) {  // the last knot record of the phase, if still waiting
-          real r[RING_W];
-          const int kk = N - 2, sl = (s - 1) & (RD - 1);
+  };
+  // cost side, phase constants: ReB parameters and the staged position references
+  struct CostPhase {
+    real delta, etq, egr, refT;
+    bool sref;
+    const real* refpos;
+  };
+  auto cost_phase_begin = [&](int p) {
+    CostPhase c;
+    const int N = sp.N[p], ko = sp.ko[p];
+    const bool wb = p < sp.n_wb;
+    c.delta = c.etq = c.egr = real(0.0);
+    if (run && wb) { c.delta = st->delta[p]; c.etq = st->eps_tq[p]; c.egr = st->eps_grf[p]; }
+    c.refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
+    // position references of the phase: staged in LDS by the cost side (one round trip per
+    // phase), read from HBM per knot when the phase is longer than the stage
+    c.sref = ST && N <= ST_RMAX;
+    if (c.sref) {
 #pragma unroll
-          for (int i = 0; i < RING_W; ++i) r[i] = i < nrec ? ring[sl][i][lane] : real(0.0);
-          const real pos = sref ? sRef[lp][kk] : refpos[kk];
-          V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, delta, etq, egr)
-                  : fb_running_cost(sp, mode, dt, pos, r, r + 6);
-          store_rec(r, nrec, ko + kk);
-        }
-        if (PIPE) {
+      for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
+        const int fi = lane + 64 * i, rl = fi / ST_RMAX, rk = fi - rl * ST_RMAX;
+        if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
+      }
+    }
+    c.refT = run ? (c.sref ? sRef[lp][N - 1] : c.refpos[N - 1]) : real(0.0);
+    return c;
+  };
+  // cost side: the running cost of knot kk from record r (knot order: the serial rollout's
+  // association) and the record's store
+  auto cost_knot = [&](int p, const CostPhase& c, int kk, const real* r, acc& V) {
+    const int mode = sp.mode[p], ko = sp.ko[p];
+    const real dt = sp.dt[p];
+    const bool wb = p < sp.n_wb;
+    const real pos = c.sref ? sRef[lp][kk] : c.refpos[kk];
+    V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, c.delta, c.etq, c.egr)
+            : fb_running_cost(sp, mode, dt, pos, r, r + 6);
+    store_rec(r, wb ? RING_W : 14, ko + kk);
+  };
+  auto ring_rec = [&](int sl, real* r, int n) {
 #pragma unroll
-          for (int i = 0; i < RING_W; ++i) xe[i] = i < nx ? ring[s][i][lane] : real(0.0);
+    for (int i = 0; i < RING_W; ++i) r[i] = i < n ? ring[sl][i][lane] : real(0.0);
+  };
+  // cost side, phase end: terminal cost, touchdown constraint, AL term (SinglePhase.cpp
+  // :251-275), the phase value into sV / sH and the terminal record's store
+  auto cost_terminal = [&](int p, const CostPhase& c, const real* xe, acc V) {
+    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const bool wb = p < sp.n_wb;
+    real h = 0;
+    if (wb) {
+      real rx[14];
+      wb_term_ref(sp, mode, c.refT, rx);
+      acc Phi = 0;
+      for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
+      Phi = Phi * acc(0.5);
+      if (ntc_of(mode, true)) {
+        h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
+        if (sp.AL_active) {
+          const acc sg = st->sigma[p], lam = st->lambda[p];
+          const acc sh2 = sg * h / 2;
+          Phi += 50 * (sh2 * sh2 + lam * h);
         }
-        real h = 0;
-        if (wb) {
-          real rx[14];
-          wb_term_ref(sp, mode, refT, rx);
-          acc Phi = 0;
-          for (int i = 0; i < 14; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.wQf[mode - 1][i] * e; }
-          Phi = Phi * acc(0.5);
-          if (ntc_of(mode, true)) {
-            h = mode == 2 ? wb_touchdown_value<kFront>(xe) : wb_touchdown_value<kBack>(xe);
-            if (sp.AL_active) {
-              const acc sg = st->sigma[p], lam = st->lambda[p];
-              const acc sh2 = sg * h / 2;
-              Phi += 50 * (sh2 * sh2 + lam * h);
+      }
+      V += Phi;
+    } else {
+      real rx[6];
+      fb_term_ref(sp, c.refT, rx);
+      acc Phi = 0;
+      for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
+      V += Phi * acc(0.5);
+    }
+    J += V;
+    viol2 += acc(h) * h;
+    sV[p][lane] = V;
+    sH[p][lane] = h;
+    store_rec(xe, wb ? 14 : 6, ko + N - 1);
+  };
+
+  if constexpr (PIPE) {
+    // Two waves on the same (problem, candidate) lanes, each in its own loop (disjoint
+    // register live ranges): wave 0 rolls out and hands each knot record over through a
+    // ring of RD records, wave 1 takes them RG at a time after a barrier.  Both loops walk the
+    // same record sequence, so their barriers pair up.
+    int q = 0;
+    if (w0) {
+      for (int p = 0; p < sp.P; ++p) {
+        const int N = sp.N[p], ko = sp.ko[p];
+        const bool wb = p < sp.n_wb;
+        const int nx = wb ? 14 : 6;
+        dyn_phase_begin(p);
+        for (int k = 0; k < N - 1; ++k, ++q) {
+          const int s = q & (RD - 1);
+          const bool bar = (q & (RG - 1)) == RG - 1;
+          real rr[RING_W];
+          const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+          RO_T(tk0);
+          if (ST && !PF && (k & (CH - 1)) == 0) chunk_turn(wb, ko, N, k);
+          RO_T(tkc);
+          if (run) dyn_knot(p, k, rr);
+          RO_T(tk2);
+          if (PF && k + 1 < N - 1) {
+            if (((k + 1) & (CH - 1)) == 0) chunk_turn(wb, ko, N, k + 1);
+            if (run) prefetch(wb, k + 1);
+          }
+          if (run) {
+            if (PAIR) {
+              // WB: x half (7), u pair (2), y pair (2); SRB: half of the 14 entries
+              if (wb) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
+                ring[s][back ? 16 : 14][cl] = rr[7];
+                ring[s][back ? 17 : 15][cl] = rr[8];
+                ring[s][back ? 20 : 18][cl] = rr[9];
+                ring[s][back ? 21 : 19][cl] = rr[10];
+              } else {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) ring[s][(back ? 7 : 0) + i][cl] = rr[i];
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < RING_W; ++i)
+                if (i < (wb ? RING_W : 14)) ring[s][i][lane] = rr[i];
             }
           }
-          V += Phi;
-        } else {
-          real rx[6];
-          fb_term_ref(sp, refT, rx);
-          acc Phi = 0;
-          for (int i = 0; i < 6; ++i) { const real e = xe[i] - rx[i]; Phi += e * sp.cw.fQf[mode - 1][i] * e; }
-          V += Phi * acc(0.5);
+          if (bar) __syncthreads();
+#ifdef MHPC_RO_TIMING
+          if (lane == 0 && run) {
+            const unsigned long long tk3 = clock64();
+            ro_cyc[wb ? 1 : 7] += tk2 - tkc;
+            ro_cyc[wb ? 2 : 8] += tk3 - tk2;
+            ro_cyc[9] += tkc - tk0;
+            if (wb) ro_cyc[4]++; else { ro_cyc[5]++; ro_cyc[3] += tk3 - tk0; }
+          }
+#endif
         }
-        J += V;
-        viol2 += acc(h) * h;
-        sV[p][lane] = V;
-        sH[p][lane] = h;
-        store_rec(xe, nx, ko + N - 1);
+        // the phase's terminal state into the ring, then the transition
+        const int s = q & (RD - 1);
+        ++q;
+        if (run) {
+          if (PAIR) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+              const int e = (back ? 7 : 0) + i;
+              if (e < nx) ring[s][e][cl] = back ? x[7 + i] : x[i];
+            }
+          } else {
+            for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
+          }
+          transition(p);
+        }
+        __syncthreads();
+      }
+    } else {
+      for (int p = 0; p < sp.P; ++p) {
+        const int N = sp.N[p];
+        const bool wb = p < sp.n_wb;
+        const int nrec = wb ? RING_W : 14;
+        const CostPhase c = cost_phase_begin(p);
+        acc V = 0;
+        int pend = -1;  // a knot record handed over but not consumed yet (RG > 1)
+        for (int k = 0; k < N - 1; ++k, ++q) {
+          const int s = q & (RD - 1);
+          const bool bar = (q & (RG - 1)) == RG - 1;
+          if (bar) {
+#ifdef MHPC_RO_TIMING
+            const unsigned long long ta = lane == 0 ? clock64() : 0ull;
+#endif
+            __syncthreads();
+#ifdef MHPC_RO_TIMING
+            const unsigned long long tb = lane == 0 ? clock64() : 0ull;
+#endif
+            if (run) {
+              real r[RING_W];
+              if (RG > 1 && pend >= 0) {
+                ring_rec((s - 1) & (RD - 1), r, nrec);
+                cost_knot(p, c, pend, r, V);
+              }
+              ring_rec(s, r, nrec);
+              cost_knot(p, c, k, r, V);
+            }
+#ifdef MHPC_RO_TIMING
+            if (lane == 0 && run) {  // cost wave: barrier wait, consume time per WB / SRB record
+              const unsigned long long tc = clock64() + (unsigned long long)(V != V);
+              ro_cyc[10] += tb - ta;
+              ro_cyc[wb ? 0 : 6] += tc - tb;
+            }
+#endif
+          }
+          if (RG > 1) pend = bar ? -1 : k;  // RG = 2: at most one record waits
+        }
+        const int s = q & (RD - 1);
+        ++q;
+        __syncthreads();
+        if (run) {
+          real r[RING_W];
+          if (RG > 1 && pend >= 0) {  // the phase's last knot record, if still waiting
+            ring_rec((s - 1) & (RD - 1), r, nrec);
+            cost_knot(p, c, N - 2, r, V);
+          }
+          ring_rec(s, r, wb ? 14 : 6);
+          cost_terminal(p, c, r, V);
+        }
+      }
+    }
+  } else {
+    // one wave: the rollout and the costs of each knot in turn (records in registers)
+    for (int p = 0; p < sp.P; ++p) {
+      const int N = sp.N[p], ko = sp.ko[p];
+      const bool wb = p < sp.n_wb;
+      const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+      dyn_phase_begin(p);
+      const CostPhase c = cost_phase_begin(p);
+      acc V = 0;
+      for (int k = 0; k < N - 1; ++k) {
+        if (ST && (k & (CH - 1)) == 0) chunk_turn(wb, ko, N, k);
+        if (run) {
+          real rr[RING_W];
+          dyn_knot(p, k, rr);
+          if (!wb) {
+#pragma unroll
+            for (int i = 6; i < RING_W; ++i) rr[i] = i < 14 ? rr[i] : real(0.0);
+          }
+          cost_knot(p, c, k, rr, V);
+        }
+      }
+      if (run) {
+        real xe[RING_W];
+#pragma unroll
+        for (int i = 0; i < RING_W; ++i) xe[i] = i < (wb ? 14 : 6) ? x[i] : real(0.0);
+        transition(p);
+        cost_terminal(p, c, xe, V);
       }
     }
   }
@@ -525,7 +653,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   }
   __syncthreads();
 #ifdef MHPC_RO_TIMING
-  if (lane == 0 && w0)
+  if (lane == 0)
     for (int i = 0; i < 11; ++i) atomicAdd(&g_ro_cyc[i], ro_cyc[i]);
 #endif
   if (full) {

@@ -24,9 +24,10 @@ for it in range(2):
 c = list(buf)
 nw, nf = max(c[4], 1), max(c[5], 1)
 print("batch", B, "knots timed (lane 0 of each dynamics wave): WB", c[4], "SRB", c[5])
-for name, v, n in [("WB feedback u", c[0], nw), ("WB dynamics", c[1], nw),
-                   ("WB hand-over", c[2], nw), ("SRB knot", c[3], nf),
-                   ("SRB feedback u", c[6], nf), ("SRB dynamics", c[7], nf), ("SRB hand-over", c[8], nf),
-                   ("chunk stage", c[9], nw + nf), ("  of it: drop", c[10], nw + nf)]:
-    print(f"{name:14s} {v / n:9.1f} cyc/knot")
-print(f"{'WB total':14s} {sum(c[:3]) / nw:9.1f} cyc/knot")
+for name, v, n in [("WB fb + dynamics", c[1], nw), ("WB hand-over", c[2], nw),
+                   ("SRB knot", c[3], nf), ("SRB fb + dynamics", c[7], nf),
+                   ("SRB hand-over", c[8], nf), ("chunk stage", c[9], nw + nf),
+                   ("cost wave: WB record", c[0], nw), ("cost wave: SRB record", c[6], nf),
+                   ("cost wave: barrier wait", c[10], nw + nf)]:
+    print(f"{name:24s} {v / n:9.1f} cyc/knot")
+print(f"{'WB total (dynamics wave)':24s} {sum(c[1:3]) / nw:9.1f} cyc/knot")
