@@ -83,7 +83,7 @@ static __device__ __forceinline__ void reduced_barrier(real g, real delta, real*
 static __device__ real wb_running_cost(const SolveParams& sp, int mode, real dt, real pos,
                                   const real* x, const real* u, const real* y, bool reb,
                                   real delta, real eps_tq, real eps_grf) {
-  MHPC_NO_FMA_F32
+  MHPC_NO_FMA_COST
   const int m = mode - 1;
   real rx[14] = {pos, sp.height, 0, cQjointBias[0], cQjointBias[1], cQjointBias[2],
                    cQjointBias[3], sp.vel, 0, 0, 0, 0, 0, 0};
@@ -124,7 +124,7 @@ static __device__ real wb_running_cost(const SolveParams& sp, int mode, real dt,
 
 static __device__ real fb_running_cost(const SolveParams& sp, int mode, real dt, real pos,
                                   const real* x, const real* u) {
-  MHPC_NO_FMA_F32
+  MHPC_NO_FMA_COST
   const int m = mode - 1;
   const real rx[6] = {pos, sp.height, 0, sp.vel, 0, 0};
   const real ru[4] = {0, kGRF, 0, kGRF};

@@ -34,6 +34,14 @@
 #else
 #define MHPC_NO_FMA_F32
 #endif
+// Costs and their sums, in both precisions: a cost evaluation is inlined into the loops of
+// several kernels (line search, forward_sweep(0), trial rollouts) and its last product could
+// otherwise fuse with the caller's accumulation in one of them and not in another.
+#if defined(__clang__)
+#define MHPC_NO_FMA_COST _Pragma("clang fp contract(off)")
+#else
+#define MHPC_NO_FMA_COST
+#endif
 
 namespace MHPC_NS {
 

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mhpc_device.h"
 #include "mhpc_model_pair.h"
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   acc J = 0, viol2 = 0;
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
-  auto store_rec = [&](const real* r, int n, int kk) {
+  auto store_rec = [&](const real* r, int n, int kk) __attribute__((always_inline)) {
     real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
     for (int i = 0; i < RING_W / 2; ++i)
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // the hand-over instead of heading the next knot's dependent chain; the next chunk is
   // dropped into the stage right after the last knot of a chunk has read it.
   real pK[28], pX[14], pU[4], pD[4];
-  auto prefetch = [&](bool wb, int kk) {
+  auto prefetch = [&](bool wb, int kk) __attribute__((always_inline)) {
     const int kcc = kk & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
     const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
     const int D0 = wb ? Stage<true>::D0 : Stage<false>::D0;
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // drop the loaded chunk (knots k1..) into the stage and fetch the next one (all lanes of
   // the dynamics wave: the loads are cooperative)
-  auto chunk_turn = [&](bool wb, int ko, int N, int k1) {
+  auto chunk_turn = [&](bool wb, int ko, int N, int k1) __attribute__((always_inline)) {
     const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
     stage_drop<SNP>(lane, pf, stage2);
     if (k1 + CH < N - 1) {
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     }
   };
   // dynamics side, phase start: SRB foothold / contact, first chunk of the stage
-  auto dyn_phase_begin = [&](int p) {
+  auto dyn_phase_begin = [&](int p) __attribute__((always_inline)) {
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
     const bool wb = p < sp.n_wb;
     if (run && !wb) {
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // dynamics side, knot k of phase p: u = (u_nom + eps du) + K (x - x_nom), x+ = x + dt f(x, u);
   // rr = the knot's record (x, u, y) as the ring / the cost side takes it
-  auto dyn_knot = [&](int p, int k, real* rr) {
+  auto dyn_knot = [&](int p, int k, real* rr) __attribute__((always_inline)) {
     const int mode = sp.mode[p], ko = sp.ko[p];
     const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     }
   };
   // phase transition after the phase's terminal state (MultiPhaseDDP.cpp:351-379)
-  auto transition = [&](int p) {
+  auto transition = [&](int p) __attribute__((always_inline)) {
     const int mode = sp.mode[p];
     if (p < sp.n_wb && p + 1 < sp.P) {
       if (mode == 2 || mode == 4) {
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     bool sref;
     const real* refpos;
   };
-  auto cost_phase_begin = [&](int p) {
+  auto cost_phase_begin = [&](int p) __attribute__((always_inline)) {
     CostPhase c;
     const int N = sp.N[p], ko = sp.ko[p];
     const bool wb = p < sp.n_wb;
@@ -443,7 +444,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // cost side: the running cost of knot kk from record r (knot order: the serial rollout's
   // association) and the record's store
-  auto cost_knot = [&](int p, const CostPhase& c, int kk, const real* r, acc& V) {
+  auto cost_knot = [&](int p, const CostPhase& c, int kk, const real* r, acc& V) __attribute__((always_inline)) {
+    MHPC_NO_FMA_COST
     const int mode = sp.mode[p], ko = sp.ko[p];
     const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
@@ -452,13 +454,14 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
             : fb_running_cost(sp, mode, dt, pos, r, r + 6);
     store_rec(r, wb ? RING_W : 14, ko + kk);
   };
-  auto ring_rec = [&](int sl, real* r, int n) {
+  auto ring_rec = [&](int sl, real* r, int n) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < RING_W; ++i) r[i] = i < n ? ring[sl][i][lane] : real(0.0);
   };
   // cost side, phase end: terminal cost, touchdown constraint, AL term (SinglePhase.cpp
   // :251-275), the phase value into sV / sH and the terminal record's store
-  auto cost_terminal = [&](int p, const CostPhase& c, const real* xe, acc V) {
+  auto cost_terminal = [&](int p, const CostPhase& c, const real* xe, acc V) __attribute__((always_inline)) {
+    MHPC_NO_FMA_COST
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
     const bool wb = p < sp.n_wb;
     real h = 0;
@@ -498,10 +501,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     // same record sequence, so their barriers pair up.
     int q = 0;
     if (w0) {
-      for (int p = 0; p < sp.P; ++p) {
+      // one copy of the knot loop per phase kind (WB / SRB): no joins of the two kinds'
+      // registers inside the loop (those forced the prefetched operands to land early)
+      auto dyn_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
+        constexpr bool wb = decltype(WBc)::value;
         const int N = sp.N[p], ko = sp.ko[p];
-        const bool wb = p < sp.n_wb;
-        const int nx = wb ? 14 : 6;
+        constexpr int nx = wb ? 14 : 6;
         dyn_phase_begin(p);
         for (int k = 0; k < N - 1; ++k, ++q) {
           const int s = q & (RD - 1);
@@ -564,12 +569,16 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           transition(p);
         }
         __syncthreads();
+      };
+      for (int p = 0; p < sp.P; ++p) {
+        if (p < sp.n_wb) dyn_phase(std::true_type{}, p);
+        else dyn_phase(std::false_type{}, p);
       }
     } else {
-      for (int p = 0; p < sp.P; ++p) {
+      auto cost_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
+        constexpr bool wb = decltype(WBc)::value;
         const int N = sp.N[p];
-        const bool wb = p < sp.n_wb;
-        const int nrec = wb ? RING_W : 14;
+        constexpr int nrec = wb ? RING_W : 14;
         const CostPhase c = cost_phase_begin(p);
         acc V = 0;
         int pend = -1;  // a knot record handed over but not consumed yet (RG > 1)
@@ -615,6 +624,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           ring_rec(s, r, wb ? 14 : 6);
           cost_terminal(p, c, r, V);
         }
+      };
+      for (int p = 0; p < sp.P; ++p) {
+        if (p < sp.n_wb) cost_phase(std::true_type{}, p);
+        else cost_phase(std::false_type{}, p);
       }
     }
   } else {
@@ -756,20 +769,23 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
 #pragma unroll
         for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
       }
-      real rx[14];
-      wb_term_ref(sp, mode, refpos[N - 1], rx);
-      acc Phi = 0;
-      for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.wQf[mode - 1][i] * ee; }
-      Phi = Phi * acc(0.5);
-      if (ntc_of(mode, true)) {
-        h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
-        if (sp.AL_active) {
-          const acc sg = st->sigma[p], lam = st->lambda[p];
-          const acc sh2 = sg * h / 2;
-          Phi += 50 * (sh2 * sh2 + lam * h);
+      {
+        MHPC_NO_FMA_COST
+        real rx[14];
+        wb_term_ref(sp, mode, refpos[N - 1], rx);
+        acc Phi = 0;
+        for (int i = 0; i < 14; ++i) { const real ee = x[i] - rx[i]; Phi += ee * sp.cw.wQf[mode - 1][i] * ee; }
+        Phi = Phi * acc(0.5);
+        if (ntc_of(mode, true)) {
+          h = mode == 2 ? wb_touchdown_value<kFront>(x) : wb_touchdown_value<kBack>(x);
+          if (sp.AL_active) {
+            const acc sg = st->sigma[p], lam = st->lambda[p];
+            const acc sh2 = sg * h / 2;
+            Phi += 50 * (sh2 * sh2 + lam * h);
+          }
         }
+        V += Phi;
       }
-      V += Phi;
       if (p + 1 < sp.P) {
         if (mode == 2 || mode == 4) {
           real xp[14], lam[2];
@@ -1259,6 +1275,7 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   }
   __syncthreads();
   if (lane < sp.P) {
+    MHPC_NO_FMA_COST
     const int p = lane, mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
     acc V = 0;
     real h = 0;
