@@ -631,11 +631,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       }
     }
   } else {
-    // one wave: the rollout and the costs of each knot in turn (records in registers)
-    for (int p = 0; p < sp.P; ++p) {
+    // one wave: the rollout and the costs of each knot in turn (records in registers), one
+    // copy of the knot loop per phase kind
+    auto fused_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
+      constexpr bool wb = decltype(WBc)::value;
       const int N = sp.N[p], ko = sp.ko[p];
-      const bool wb = p < sp.n_wb;
-      const int CH = wb ? Stage<true>::CH : Stage<false>::CH;
+      constexpr int CH = wb ? Stage<true>::CH : Stage<false>::CH;
       dyn_phase_begin(p);
       const CostPhase c = cost_phase_begin(p);
       acc V = 0;
@@ -658,6 +659,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         transition(p);
         cost_terminal(p, c, xe, V);
       }
+    };
+    for (int p = 0; p < sp.P; ++p) {
+      if (p < sp.n_wb) fused_phase(std::true_type{}, p);
+      else fused_phase(std::false_type{}, p);
     }
   }
   if (w1 && run) {
