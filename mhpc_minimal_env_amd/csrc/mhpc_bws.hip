@@ -264,6 +264,22 @@ __device__ __forceinline__ bool ldlt_is_positive4(real* A) {
 #ifndef MHPC_BWS_PSD
 #define MHPC_BWS_PSD 1
 #endif
+// MHPC_BWS_PSD_RCP (A/B): the pivots' reciprocals by the hardware estimate and two Newton
+// steps (<= 1 ulp) instead of IEEE divisions -- the verdict only reads signs.
+#ifndef MHPC_BWS_PSD_RCP
+#define MHPC_BWS_PSD_RCP 0
+#endif
+__device__ __forceinline__ real fast_recip(real a) {
+#if MHPC_BWS_PSD_RCP
+  real r = __builtin_amdgcn_rcp(a);
+  real e = fma(-a, r, real(1.0));
+  r = fma(r, e, r);
+  e = fma(-a, r, real(1.0));
+  return fma(r, e, r);
+#else
+  return real(1.0) / a;
+#endif
+}
 __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
   bool neg = false;
 #pragma unroll
@@ -271,7 +287,7 @@ __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
     const real akk = A[k * 5];
     neg = neg || akk < real(0.0);
     const bool valid = akk != real(0.0);
-    const real r = real(1.0) / (valid ? akk : real(1.0));
+    const real r = fast_recip(valid ? akk : real(1.0));
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
       const real l = A[i * 4 + k] * r;

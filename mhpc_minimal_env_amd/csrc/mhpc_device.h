@@ -64,18 +64,25 @@ static __device__ __forceinline__ real log_pos(real x) {
 // The reference's pow() calls with integer exponents are evaluated exactly as products:
 // pow(t, 2) = t*t (the correctly rounded square), pow(t, 1) = t, pow(t, 0) = 1 (also for
 // NaN, as pow defines), pow(g, -2) = 1/(g*g) (within 1 ulp of the correctly rounded value).
-// Branch-free: one log per constraint (of g or of delta, whichever branch the lane takes)
-// instead of both sides of a divergent branch; each lane computes exactly the operations of
-// its branch.
+// One log per constraint (of g or of delta, whichever side the lane takes) outside the branch,
+// so a wave whose lanes split over the two sides evaluates one log, not both; the relaxed
+// side's extra work stays behind a branch that waves far from the constraint skip.  Each lane
+// computes exactly the operations of its side.
 static __device__ __forceinline__ void reduced_barrier(real g, real delta, real* B, real* Bz,
                                                 real* Bzz) {
   MHPC_NO_FMA_F32
   const bool in = g > delta;
   const real lg = log_pos(in ? g : delta);
-  const real t = (g - 2 * delta) / ((2 - 1) * delta);
-  *B = in ? -lg : (real)(2 - 1) / 2 * (t * t - 1) - lg;
-  *Bz = in ? -1.0 / g : t / delta;
-  *Bzz = in ? 1.0 / (g * g) : real(1.0);
+  if (in) {
+    *B = -lg;
+    *Bz = -1.0 / g;
+    *Bzz = 1.0 / (g * g);
+  } else {
+    const real t = (g - 2 * delta) / ((2 - 1) * delta);
+    *B = (real)(2 - 1) / 2 * (t * t - 1) - lg;
+    *Bz = t / delta;
+    *Bzz = 1.0;
+  }
 }
 
 // Running cost value incl. the ReB barrier of WB phases (CostBase.cpp:4-16,
