@@ -1,0 +1,64 @@
+"""Bitwise comparison of two builds of the library on the same solves (a kernel rewrite that
+must not change a single rounding).  Each build runs in its own process (MHPC_AMD_LIB):
+
+  python tools/lib_bitwise.py dump <out.npz> <workload> <batch> [bws variant] [precision]
+  python tools/lib_bitwise.py cmp <a.npz> <b.npz>
+
+Dump: C3 / C5 initial states of configs.x0_for, one full solve (every variant choice left
+automatic unless given), all per-knot outputs and scalars.  Cmp: exact equality (+0 == -0)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+KEYS = ("X", "U", "Y", "K", "DU", "G", "J", "dV_exp", "viol", "V", "dV", "trace", "status")
+
+
+def dump(out, workload, batch, bws="auto", precision=64):
+    from mhpc_minimal_env_amd import configs, locomotion as L
+    desc = configs.c5_desc(int(precision)) if workload == "c5" else configs.c3_desc()
+    x0 = configs.x0_for(desc, batch)
+    loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=batch, device=0)
+    try:
+        loco.set_kernel_variant(bws=bws)
+        loco.set_initial_condition(x0)
+        loco.initialization()
+        status = loco.solve_mhpc().copy()
+        res = loco.concatenated()
+        res.update(loco.get_scalars())
+        res["status"] = status
+    finally:
+        loco.close()
+    np.savez(out, **{k: np.asarray(res[k]) for k in KEYS})
+
+
+def cmp(a, b):
+    A, B = np.load(a), np.load(b)
+    bad = []
+    for k in KEYS:
+        x, y = A[k], B[k]
+        if x.shape != y.shape:
+            bad.append(f"{k}: shape {x.shape} vs {y.shape}")
+            continue
+        eq = (x == y) | (np.isnan(x) & np.isnan(y)) if x.dtype.kind == "f" else x == y
+        if not eq.all():
+            n = int((~eq).sum())
+            if x.dtype.kind == "f":
+                d = np.abs(x.astype(float) - y.astype(float))[~eq]
+                rel = d / np.maximum(1.0, np.abs(y.astype(float))[~eq])
+                bad.append(f"{k}: {n} of {x.size} differ, max abs {d.max():.3e}, max rel {rel.max():.3e}")
+            else:
+                bad.append(f"{k}: {n} of {x.size} differ")
+    print(f"{a} vs {b}:", "BITWISE EQUAL" if not bad else "DIFFER")
+    for l in bad:
+        print("  " + l)
+    return not bad
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "dump":
+        dump(sys.argv[2], sys.argv[3], int(sys.argv[4]), *(sys.argv[5:]))
+    else:
+        sys.exit(0 if cmp(sys.argv[2], sys.argv[3]) else 1)
