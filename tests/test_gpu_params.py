@@ -63,6 +63,47 @@ def test_modified_params_vs_oracle(need_gpu, name):
     assert_oracle(got, ref, SOLVE_TOL)
 
 
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_zero_control_weights_vs_oracle(need_gpu, name):
+    """No control / force-rate cost (R = 0, S = 0 in every mode): Quu is B'HB (+ D'lyyD), so
+    the PSD test of the sweep decides on nearly singular blocks.  The device's unpivoted
+    LDL^T verdict (mhpc_bws.hip) against the oracle's pivoted one (Eigen's LDLT): the same
+    regularisation retries in every DDP iteration (decision traces identical; C5 iterations
+    sweep up to six times) and the same solves."""
+    import oracle as O
+    from mhpc_minimal_env_amd import capi, configs, locomotion as L
+    desc = configs.c3_desc() if name == "c3" else configs.c5_desc(64)
+    x0 = configs.x0_for(desc, 64, offset=777)
+    w = capi.default_cost_weights()
+    for m in range(4):
+        for i in range(4):
+            w.wb_R[m][i] = w.fb_R[m][i] = w.wb_S[m][i] = 0.0
+    got = solve(desc, x0, w)
+    if not O.available():
+        pytest.skip("oracle not built")
+    try:
+        O.set_params(w, None)
+        ref = O.solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=8)
+    finally:
+        O.set_params(None, None)
+    retries = [e["n_bws"] for row in np.asarray(got["trace"]) for e in O.decode_trace(row)]
+    assert sum(n > 1 for n in retries) > 0  # the PSD test rejected sweeps
+    np.testing.assert_array_equal(got["trace"], ref["trace"])
+    np.testing.assert_array_equal(got["status"], ref["status"])
+    # without a control cost the gains are ill-conditioned: the model's ~1e-11 rounding
+    # differences from the CasADi kernels grow to ~1e-5 in K (every decision identical);
+    # the costs and the value function stay at the solve tolerance
+    err = {}
+    for k in ("X", "U", "Y", "K", "DU", "G", "J", "dV_exp", "viol", "V", "dV"):
+        a, b = np.asarray(got[k], float), np.asarray(ref[k], float)
+        err[k] = float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
+    print(name, "max relative error", {k: f"{v:.1e}" for k, v in err.items()})
+    for k in ("J", "V", "dV", "viol"):
+        assert err[k] <= SOLVE_TOL, (k, err[k])
+    for k, v in err.items():
+        assert v <= 1e-3, (k, v)
+
+
 def test_modified_params_every_variant_bitwise(need_gpu):
     from mhpc_minimal_env_amd import configs
     w, c = modified_params()
