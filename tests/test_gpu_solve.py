@@ -274,3 +274,30 @@ def test_shortest_phases_vs_oracle_and_variants(need_gpu, Ns):
     for bws, ro, ov in ALL_VARIANTS:
         assert_bitwise(solve(desc, x0, bws=bws, rollout=ro, overlap=ov), base,
                        f"N={Ns}, bws={bws} rollout={ro} overlap={ov}")
+
+
+OPTION_CASES = {
+    "no_AL_no_ReB": dict(AL_active=False, ReB_active=False),
+    "AL_only": dict(ReB_active=False),
+    "long_schedule": dict(max_AL_iter=4, max_DDP_iter=6, DDP_thresh=1e-6, AL_thresh=1e-5),
+    "penalty_schedule": dict(update_penalty=2, update_relax=0.5, update_ReB=3,
+                             update_regularization=5),
+}
+
+
+@pytest.mark.parametrize("case", sorted(OPTION_CASES))
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_hsddp_options_vs_oracle(need_gpu, name, case):
+    """HSDDP_OPTION beyond the defaults (MultiPhaseDDP.cpp:154-289: AL / ReB switched off, a
+    longer AL x DDP schedule with tighter thresholds, other penalty / relaxation / ReB /
+    regularisation updates) against the oracle solving with the same option."""
+    O = _oracle()
+    if O is None:
+        pytest.skip("oracle not built on this machine")
+    from mhpc_minimal_env_amd import configs, locomotion as L
+    desc = getattr(configs, f"{name}_desc")()
+    opt = L.HSDDP_OPTION(**OPTION_CASES[case])
+    x0 = configs.x0_for(desc, 16 if name == "c3" else 4, offset=555)
+    got = run_gpu(desc, opt, x0)
+    errs = compare(got, O.solve(desc, opt.to_c(), x0, nthreads=8))
+    print(name, case, {k: f"{v:.2e}" for k, v in errs.items()})
