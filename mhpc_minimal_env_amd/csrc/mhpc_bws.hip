@@ -42,7 +42,7 @@ constexpr int QR = 24;          // rows of Q (padded)
 // leading pad element per row), so R2 and R3 read their operand runs with ds_read_b128
 // (4 LDS cycles for 16 bytes per lane) instead of strided ds_read2_b64 pairs (8 cycles).
 // Jt row strides 18 / 10 doubles put the rows of a 16-lane b128 group on distinct banks
-// (tools/lds_bank_model.py).  Only the LDS layout changes: same products, same order.
+// (tools/lds_bank_model_r3.py).  Only the LDS layout changes: same products, same order.
 #ifndef MHPC_BWS_WT
 #define MHPC_BWS_WT 1
 #endif
@@ -61,13 +61,15 @@ constexpr int JtOff = MHPC_BWS_WT ? 1 : 0;
 #ifndef MHPC_BWS_UT
 #define MHPC_BWS_UT 1
 #endif
-// Row stride of Q for the WB knot and column stride of U (bank spreading of R3's writes and
-// R5's reads: tools/lds_bank_model.py)
+// Row stride of Q for the WB knot and column stride of U: bank spreading of R3's stores and
+// R45's reads (tools/lds_bank_model_r3.py models every access of the whole-body knot: 575 ->
+// 543 LDS-array cycles at 31 / 10 against 22 / 4; measured at batch 4096, k_bws<64,2,2>
+// SQ_LDS_BANK_CONFLICT -18 %, SQ_LDS_IDX_ACTIVE -4.3 %, profiles/r03_bank_strides.txt)
 #ifndef MHPC_BWS_QS14
-#define MHPC_BWS_QS14 22
+#define MHPC_BWS_QS14 31
 #endif
 #ifndef MHPC_BWS_US
-#define MHPC_BWS_US 4
+#define MHPC_BWS_US 10
 #endif
 template <int NX> struct QShape {
   static constexpr int NR = NX + 4;
