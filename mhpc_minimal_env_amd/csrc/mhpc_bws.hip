@@ -46,7 +46,10 @@ constexpr int QR = 24;          // rows of Q (padded)
 #ifndef MHPC_BWS_WT
 #define MHPC_BWS_WT 1
 #endif
-constexpr int WR = 8;  // column stride of W (MHPC_BWS_WT)
+#ifndef MHPC_BWS_WR
+#define MHPC_BWS_WR 8
+#endif
+constexpr int WR = MHPC_BWS_WR;  // column stride of W (MHPC_BWS_WT)
 __device__ __forceinline__ constexpr int widx(int r, int col) {
   return MHPC_BWS_WT ? col * WR + r : r * WS + col;
 }

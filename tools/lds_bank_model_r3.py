@@ -41,7 +41,7 @@ def layout(QS, JTS, US, HS=14):
         o = (o + al - 1) // al * al
         off[name] = o
         o += n
-    f("H", 14 * HS, 2); f("G", 14, 2); f("W", 24 * 8, 2); f("G2", 48, 2); f("l", 24); f("ldiag", 18)
+    f("H", 14 * HS, 2); f("G", 14, 2); f("W", 28 * 14, 2); f("G2", 48, 2); f("l", 24); f("ldiag", 18)
     f("lyy2", 4); f("ly2", 2)
     u0 = (o + 1) // 2 * 2
     off["Jt"] = u0; off["Q"] = u0 + 24 * JTS; off["U"] = (off["Q"] + 24 * QS + 1) // 2 * 2
@@ -51,10 +51,17 @@ def layout(QS, JTS, US, HS=14):
     return off
 
 
-def model(QS=22, JTS=18, US=4, HS=14, verbose=True):
-    NQ, NX, NR = 7, 14, 18
+def model(QS=31, JTS=18, US=10, HS=14, verbose=True, NQ=7, QSF=13, JTF=10, WR=8):
+    """NQ = 7: the whole-body knot (Q row stride QS, Jt row stride JTS); NQ = 3: the SRB knot
+    (QSF, JTF; H row stride 6).  64-thread block."""
+    NX, NR = 2 * NQ, 2 * NQ + 4
     O = layout(QS, JTS, US, HS)
+    if NQ != 7:
+        QS, JTS, HS = QSF, JTF, NX
     QV = QS - 1
+    NC = NX + 1; GR = 64 // NC; T2 = -(-NR // GR)
+    RG = 64 // NR; T3 = -(-NR // RG)
+    NI = NX + 1; GC = 64 // NI; T5 = -(-NI // GC)
     res = {}
 
     def add(name, a, kind):
@@ -64,23 +71,23 @@ def model(QS=22, JTS=18, US=4, HS=14, verbose=True):
         r[2] += 1
     L = range(64)
     # R2
-    j = [l % 15 for l in L]; g = [l // 15 for l in L]
+    j = [l % NC for l in L]; g = [l // NC for l in L]
     isg = [jj == NX for jj in j]
     for r in range(NQ):
         add("R2 hc", [O["G"] + NQ + r if isg[l] else O["H"] + (NQ + r) * HS + j[l] for l in L], "r64")
-    for u in range(5):
-        row = [g[l] + 4 * u for l in L]
-        bi = [rw if rw < NQ else rw - NQ for rw in row]
-        add("R2 hb", [O["G"] + min(bi[l], 13) if isg[l] else O["H"] + min(bi[l], 13) * HS + j[l] for l in L], "r64")
-        for h in range(0, 6, 2):
-            add("R2 W", [O["W"] + row[l] * 8 + h for l in L], "r128")
-        add("R2 W", [O["W"] + row[l] * 8 + 6 for l in L], "r64")
+    for u in range(T2):
+        row = [g[l] + GR * u for l in L]
+        bi = [min(rw if rw < NQ else rw - NQ, NX - 1) for rw in row]
+        add("R2 hb", [O["G"] + bi[l] if isg[l] else O["H"] + bi[l] * HS + j[l] for l in L], "r64")
+        for h in range(0, NQ - 1, 2):
+            add("R2 W", [O["W"] + row[l] * WR + h for l in L], "r128")
+        add("R2 W", [O["W"] + row[l] * WR + NQ - 1 for l in L], "r64")
         add("R2 G2", [O["G2"] + row[l] * 2 for l in L], "r128")
         add("R2 l", [O["l"] + row[l] for l in L], "r64")
         st = []
         for l in L:
             rw = row[l]
-            if g[l] >= 4:
+            if g[l] >= GR:
                 st.append(O["junk"] + l)
             elif isg[l]:
                 st.append(O["Q"] + rw * QS + QV if rw < NX else O["U"] + QV * US + rw - NX if rw < NR else O["junk"] + l)
@@ -89,20 +96,20 @@ def model(QS=22, JTS=18, US=4, HS=14, verbose=True):
         add("R2 store", st, "w64")
     # R3
     row = [l % NR for l in L]; g = [l // NR for l in L]
-    for h in range(0, 6, 2):
+    for h in range(0, NQ - 1, 2):
         add("R3 jr", [O["Jt"] + row[l] * JTS + 1 + NQ + h for l in L], "r128")
-    add("R3 jr", [O["Jt"] + row[l] * JTS + 1 + NQ + 6 for l in L], "r64")
+    add("R3 jr", [O["Jt"] + row[l] * JTS + 1 + NQ + NQ - 1 for l in L], "r64")
     add("R3 G2row", [O["G2"] + row[l] * 2 for l in L], "r128")
     add("R3 ldiag", [O["ldiag"] + row[l] for l in L], "r64")
-    for u in range(6):
-        col = [g[l] + 3 * u for l in L]
+    for u in range(T3):
+        col = [g[l] + RG * u for l in L]
         b = [c if c < NQ else c - NQ for c in col]
         add("R3 jb", [O["Jt"] + row[l] * JTS + 1 + b[l] for l in L], "r64")
-        for h in range(0, 6, 2):
-            add("R3 W", [O["W"] + col[l] * 8 + h for l in L], "r128")
-        add("R3 W", [O["W"] + col[l] * 8 + 6 for l in L], "r64")
+        for h in range(0, NQ - 1, 2):
+            add("R3 W", [O["W"] + col[l] * WR + h for l in L], "r128")
+        add("R3 W", [O["W"] + col[l] * WR + NQ - 1 for l in L], "r64")
         add("R3 G2col", [O["G2"] + col[l] * 2 for l in L], "r128")
-        add("R3 store", [O["junk"] + l if g[l] >= 3 else
+        add("R3 store", [O["junk"] + l if g[l] >= RG else
                          (O["U"] + col[l] * US + row[l] - NX if row[l] >= NX else O["Q"] + row[l] * QS + col[l])
                          for l in L], "w64")
     # R45
@@ -115,21 +122,21 @@ def model(QS=22, JTS=18, US=4, HS=14, verbose=True):
                 a.append(O["U"] + (NX + cm) * US + rn)
             add("R45 minors", a, "r64")
     add("R45 inv store", [O["inv"] + l if l < 16 else O["junk"] + l for l in L], "w64")
-    i = [l % 15 for l in L]; g = [l // 15 for l in L]
+    i = [l % NI for l in L]; g = [l // NI for l in L]
     si = [ii if ii < NX else QV for ii in i]
     add("R45 qi", [O["U"] + si[l] * US for l in L], "r128")
     add("R45 qi", [O["U"] + si[l] * US + 2 for l in L], "r128")
     for c in range(4):
         add("R45 K store", [(O["Kst"] + c * NX + i[l] if i[l] < NX else O["dust"] + c) if g[l] == 0 else O["junk"] + l for l in L], "w64")
-    for u in range(4):
-        jj = [g[l] + 4 * u for l in L]
+    for u in range(T5):
+        jj = [g[l] + GC * u for l in L]
         sj = [x if x < NX else QV for x in jj]
         add("R45 xj", [O["U"] + sj[l] * US for l in L], "r128")
         add("R45 xj", [O["U"] + sj[l] * US + 2 for l in L], "r128")
         add("R45 qij", [O["Q"] + i[l] * QS + sj[l] for l in L], "r64")
         add("R45 qji", [O["Q"] + (jj[l] if jj[l] < NX else 0) * QS + i[l] for l in L], "r64")
         add("R45 store", [(O["H"] + i[l] * HS + jj[l] if jj[l] < NX else O["G"] + i[l])
-                          if (g[l] < 4 and i[l] < NX and jj[l] <= NX) else O["junk"] + l for l in L], "w64")
+                          if (g[l] < GC and i[l] < NX and jj[l] <= NX) else O["junk"] + l for l in L], "w64")
     tot = [sum(v[k] for v in res.values()) for k in (0, 1)]
     if verbose:
         for k, (c, ideal, n) in res.items():
@@ -141,4 +148,7 @@ def model(QS=22, JTS=18, US=4, HS=14, verbose=True):
 
 if __name__ == "__main__":
     a = [int(x) for x in sys.argv[1:5]]
+    print("whole-body knot (NQ = 7)")
     model(*a)
+    print("SRB knot (NQ = 3)")
+    model(*a, NQ=3)
