@@ -49,6 +49,12 @@ constexpr int QR = 24;          // rows of Q (padded)
 #ifndef MHPC_BWS_WR
 #define MHPC_BWS_WR 8
 #endif
+// Row stride of the whole-body knot's H (the SRB knot's 6 x 6 H stays dense): 17 puts the
+// rows R45 stores and the column R2 reads on distinct banks (tools/lds_bank_model_r3.py)
+#ifndef MHPC_BWS_HS14
+#define MHPC_BWS_HS14 14
+#endif
+template <int NX> constexpr int HStride = NX == 14 ? MHPC_BWS_HS14 : NX;
 constexpr int WR = MHPC_BWS_WR;  // column stride of W (MHPC_BWS_WT)
 __device__ __forceinline__ constexpr int widx(int r, int col) {
   return MHPC_BWS_WT ? col * WR + r : r * WS + col;
@@ -96,7 +102,7 @@ using wreal = real;
 #endif
 
 struct BwsLds {
-  alignas(16) real H[196];
+  alignas(16) real H[14 * MHPC_BWS_HS14];
   alignas(16) real G[14];  // value function of knot k+1, then of knot k (row stride NX)
   alignas(16) real W[MHPC_BWS_WT ? WS * WR : 7 * WS];  // rows NQ..NX-1 of [A B] (widx)
   alignas(16) real G2[2 * WS];                         // stance rows of [C D] (g2idx)
@@ -364,7 +370,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
     const real* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
     real hc[NQ];
 #pragma unroll
-    for (int r = 0; r < NQ; ++r) hc[r] = col0[isg ? NQ + r : (NQ + r) * NX];
+    for (int r = 0; r < NQ; ++r) hc[r] = col0[isg ? NQ + r : (NQ + r) * HStride<NX>];
     real ly0 = real(0.0), ly1 = real(0.0);
     if (HAS_Y) { ly0 = sh.ly2[0]; ly1 = sh.ly2[1]; }
     // straight-line rows (no per-row branches, so the scheduler interleaves the T2 chains):
@@ -379,7 +385,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         const int row = g + GR * (t0 + u);  // < JR
         const real a = coef_a<NQ>(row, dt);
         const int bi = coef_b<NQ>(row);
-        const real hb = col0[isg ? bi : bi * NX];
+        const real hb = col0[isg ? bi : bi * HStride<NX>];
         real sacc = a != real(0.0) ? a * hb : real(0.0);
 #pragma unroll
         for (int r = 0; r < NQ; ++r) sacc += sh.W[widx(r, row)] * hc[r];
@@ -592,7 +598,7 @@ __device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9,
         if (t0 + u >= T5) continue;
         const int j = g + GC * (t0 + u);
         const bool wr = g < GC && i < NX && j <= NX;
-        *(wr ? (j < NX ? &sh.H[i * NX + j] : &sh.G[i]) : &sh.junk[lane & 63]) = acc[u];
+        *(wr ? (j < NX ? &sh.H[i * HStride<NX> + j] : &sh.G[i]) : &sh.junk[lane & 63]) = acc[u];
       }
     }
   }
@@ -690,7 +696,7 @@ __device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLd
         const real hij = (ai >= 0 && aj >= 0) ? sh.Hs[ai * 3 + aj] : real(0.0);
         v += 50 * (s * s / 2 * (sh.hx[i] * sh.hx[j] + h * hij) + lam * hij);
       }
-      sh.H[e] = v + sh.H[e];
+      sh.H[i * HStride<NX> + j] = v + sh.H[i * HStride<NX> + j];
     } else {
       const int i = e - NX * NX;
       real rxi;
@@ -720,7 +726,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
     if (e < 196) {
       const int i = e / 14, j = e - i * 14;
       real v;
-      if (nwb) v = sh.H[e];
+      if (nwb) v = sh.H[i * HStride<14> + j];
       else {
         const int pi = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
         const int pj = j < 3 ? j : (j >= 7 && j < 10 ? j - 4 : -1);
@@ -770,11 +776,11 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsL
       real s = 0;
 #pragma unroll
       for (int m = 0; m < 14; ++m) s += sh.T[i * 14 + m] * sh.Px[m * 14 + j];
-      sh.H[e] = s;
+      sh.H[i * HStride<14> + j] = s;
     }
   } else {
     #pragma unroll 1
-    for (int e = lane; e < 196; e += NT) sh.H[e] = sh.H2[e];
+    for (int e = lane; e < 196; e += NT) sh.H[(e / 14) * HStride<14> + e % 14] = sh.H2[e];
     if (lane < 14) sh.G[lane] = sh.G2v[lane];
   }
   __syncthreads();
@@ -1021,7 +1027,7 @@ __device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbSt
     }
   } else {
     #pragma unroll 1
-    for (int e = lane; e < 196; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
+    for (int e = lane; e < 14 * MHPC_BWS_HS14; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
     if (lane < 14) sh.G[lane] = 0;
     if (lane == 0) sh.dV = 0;
   }
