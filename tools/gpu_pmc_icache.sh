@@ -1,6 +1,6 @@
 # instruction-cache and issue counters per kernel at batch $B
 set -o pipefail
-OUT=gpurun_out/pmc_icache_${B:-4096}
+OUT=gpurun_out/pmc_icache_${B:-4096}${TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
 CMD="python bench.py --steps 1 --warmup 1 --batch-per-gpu ${B:-4096} --no-cpu-baseline"
