@@ -1153,6 +1153,33 @@ __device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int
 // per-knot latency is what counts; both lanes carry the same state and controls (the pair
 // model returns xdot and y on both, bit for bit the single-lane model's), the even lane
 // writes the references and the per-problem state, each lane half of every knot record.
+// memory_reset (MHPCLocomotion.cpp:265-288), launched on the second stream beside k_init and
+// hidden behind its serial warm-start chains: K, du and G of every knot, and u and y of
+// every phase's last knot in every trajectory slot (no rollout writes them, quirk B11; a slot
+// becoming the nominal carries them into the exports).  Everything else of traj is written
+// before it is read (slot 0 by k_init, the candidate slots by the line search), so initialize
+// does not clear the whole array (2.8 GB at batch 4096).  k_init reads none of these arrays
+// and writes other elements of the tail records.
+__device__ void init_reset_arrays(const SolveParams& sp, const DevBufs& d, long t, long nt) {
+  const long nk = (long)sp.B * sp.NK;
+  for (long i = t; i < nk * 56; i += nt) d.K[i] = real(0.0);
+  for (long i = t; i < nk * 4; i += nt) d.du[i] = real(0.0);
+  for (long i = t; i < nk * 14; i += nt) d.G[i] = real(0.0);
+  const long n = (long)sp.B * sp.nslot * sp.P;
+  for (long i = t; i < n; i += nt) {
+    const int p = (int)(i % sp.P);
+    const long bs = i / sp.P;
+    const int slot = (int)(bs % sp.nslot), b = (int)(bs / sp.nslot);
+    const int nx = p < sp.n_wb ? 14 : 6;
+    real* r = traj_ptr(sp, d, b, slot, sp.ko[p] + sp.N[p] - 1);
+    for (int e = nx; e < KS; ++e) r[e] = real(0.0);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_reset_arrays(SolveParams sp, DevBufs d) {
+  init_reset_arrays(sp, d, (long)blockIdx.x * 256 + threadIdx.x, (long)gridDim.x * 256);
+}
+
 __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = t >> 1;
@@ -1456,30 +1483,15 @@ hipError_t launch_reduce_counters(const SolveParams& sp, const DevBufs& d,
   hipLaunchKernelGGL(k_reduce_counters, dim3(nb), dim3(256), 0, s, sp, d, out);
   return hipGetLastError();
 }
-// memory_reset's zeros where a solve reads them before writing: u and y of every phase's
-// last knot in every trajectory slot (no rollout writes them, quirk B11; a slot becoming the
-// nominal carries them into the exports).  Everything else of traj is written before it is
-// read (slot 0 by k_init, the candidate slots by the line search), so initialize does not
-// clear the whole array (2.8 GB at batch 4096).
-__global__ void k_zero_tails(SolveParams sp, DevBufs d) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long n = (long)sp.B * sp.nslot * sp.P;
-  if (t >= n) return;
-  const int p = (int)(t % sp.P);
-  const long bs = t / sp.P;
-  const int slot = (int)(bs % sp.nslot), b = (int)(bs / sp.nslot);
-  const int nx = p < sp.n_wb ? 14 : 6;
-  real* r = traj_ptr(sp, d, b, slot, sp.ko[p] + sp.N[p] - 1);
-  for (int i = nx; i < KS; ++i) r[i] = real(0.0);
-}
-hipError_t launch_zero_tails(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  const long n = (long)sp.B * sp.nslot * sp.P;
-  hipLaunchKernelGGL(k_zero_tails, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sp, d);
-  return hipGetLastError();
-}
-
 hipError_t launch_reset(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
   hipLaunchKernelGGL(k_init, dim3((2 * sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
+  return hipGetLastError();
+}
+hipError_t launch_reset_arrays(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
+  // ~64 elements per lane, at most 2 blocks per CU
+  const long e = (long)sp.B * sp.NK * 74 + (long)sp.B * sp.nslot * sp.P;
+  const long nb = std::min((e + 256 * 64 - 1) / (256 * 64), 2L * sp.ncu);
+  hipLaunchKernelGGL(k_reset_arrays, dim3((unsigned)nb), dim3(256), 0, s, sp, d);
   return hipGetLastError();
 }
 hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {

@@ -16,13 +16,13 @@
 
 namespace MHPC_NS {
 hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_reset_arrays(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
 bool bws_split(const SolveParams&);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
-hipError_t launch_zero_tails(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, hipStream_t);
 // N_TIMESTEPS_MAX (MHPCLocomotion.h): knots per phase buffer; record = x,u,y + K + du + G
 constexpr int kPhaseBufKnots = 110;
@@ -480,12 +480,14 @@ static int d2h(Handle* h, void* dst, const void* src, size_t bytes) {
 static int initialize_async(Handle* h) {
   const SolveParams& sp = h->sp;
   DevBufs& d = h->d;
-  const size_t B = sp.B, NK = sp.NK;
-  HIPCHK(launch_zero_tails(sp, d, h->stream));
-  HIPCHK(hipMemsetAsync(d.K, 0, B * NK * 56 * sizeof(real), h->stream));
-  HIPCHK(hipMemsetAsync(d.du, 0, B * NK * 4 * sizeof(real), h->stream));
-  HIPCHK(hipMemsetAsync(d.G, 0, B * NK * 14 * sizeof(real), h->stream));
+  // memory_reset (K / du / G, trajectory tails) on the second stream beside k_init, which
+  // touches none of it; the first solve op waits for both
+  HIPCHK(hipEventRecord(h->evfork, h->stream));
+  HIPCHK(hipStreamWaitEvent(h->stream2, h->evfork, 0));
+  HIPCHK(launch_reset_arrays(sp, d, h->stream2));
+  HIPCHK(hipEventRecord(h->evjoin, h->stream2));
   LAUNCH(h, K_INIT, launch_init(sp, d, h->stream));
+  HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
   h->kbytes[K_INIT] += h->by_init * sp.B;
   // build_problem binds phase p to buffer p; the buffer store is zeroed lazily (first
   // update_problem), so a plain initialize + solve pays nothing for it

@@ -2,13 +2,13 @@
 # C3 (automatic variant at 1024; every k_bws variant at 256) and C5 (fp64 / fp32, 64).
 # usage: REF=old bash tools/gpu_bitwise.sh
 set -o pipefail
-mkdir -p gpurun_out/bw
+BW=${BWDIR:-/tmp/bw}; mkdir -p $BW
 V=mhpc_minimal_env_amd/csrc/_build/var
 rc=0
 for cfg in "c3 1024 auto 64" "c3 256 2wave 64" "c3 256 pairwave 64" "c3 256 1wave 64" "c5 64 auto 64" "c5 64 auto 32"; do
   set -- $cfg; tag=$1_$2_$3_$4
-  MHPC_AMD_LIB=$V/${REF:-old}/libmhpc_amd.so timeout -k 10 200 python tools/lib_bitwise.py dump gpurun_out/bw/ref_$tag.npz $1 $2 $3 $4 || exit 1
-  timeout -k 10 200 python tools/lib_bitwise.py dump gpurun_out/bw/new_$tag.npz $1 $2 $3 $4 || exit 1
-  python tools/lib_bitwise.py cmp gpurun_out/bw/ref_$tag.npz gpurun_out/bw/new_$tag.npz || rc=1
+  MHPC_AMD_LIB=$V/${REF:-old}/libmhpc_amd.so timeout -k 10 200 python tools/lib_bitwise.py dump $BW/ref_$tag.npz $1 $2 $3 $4 || exit 1
+  timeout -k 10 200 python tools/lib_bitwise.py dump $BW/new_$tag.npz $1 $2 $3 $4 || exit 1
+  python tools/lib_bitwise.py cmp $BW/ref_$tag.npz $BW/new_$tag.npz || rc=1
 done
 exit $rc
