@@ -379,6 +379,10 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="N > 1 process group: nccl = RCCL over xGMI (default); gloo only for "
                          "tests on a 1-GPU box (with --share-gpu)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group even at N = 1 (runs the RCCL timing / "
+                         "all-gather / shard-check path on a one-GPU box; launch under "
+                         "torch.distributed.run)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="test only: every rank uses GPU 0 (rehearsal of the N-rank path on one GPU)")
     ap.add_argument("--bws-variant", default="auto",
@@ -416,7 +420,7 @@ def main():
         local_rank = 0
     # tensors of the timing / gather collectives live where the backend wants them
     tdev = torch.device(f"cuda:{local_rank}") if args.backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
         if args.backend == "nccl":
             torch.cuda.set_device(local_rank)
