@@ -306,7 +306,7 @@ def run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch):
                          "avg_launch_ms": per_launch_s * 1e3},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=_LINE_OUT or sys.stdout, flush=True)
     loco.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -356,6 +356,9 @@ def run_sweep(args, torch):
             "roofline": roofline_of(stats, B, args.workload),
         }), flush=True)
         s.close()
+
+
+_LINE_OUT = None  # stdout of the JSON line once library output is diverted (process group)
 
 
 def main():
@@ -421,6 +424,13 @@ def main():
     # tensors of the timing / gather collectives live where the backend wants them
     tdev = torch.device(f"cuda:{local_rank}") if args.backend == "nccl" else torch.device("cpu")
     if world > 1 or args.dist:
+        # RCCL prints a version banner on stdout when a communicator comes up; the contract's
+        # stdout is the one JSON line, so from here on library chatter goes to stderr and the
+        # line to a duplicate of the original stdout
+        global _LINE_OUT
+        sys.stdout.flush()
+        _LINE_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         import torch.distributed as dist
         if args.backend == "nccl":
             torch.cuda.set_device(local_rank)
@@ -532,7 +542,7 @@ def main():
         }
         if shard is not None:
             line["sharding"] = shard
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=_LINE_OUT or sys.stdout, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
