@@ -237,9 +237,9 @@ void mhpc_destroy(mhpc_handle* h);
  * MHPC_ERR_INVALID if the variant does not apply (the staged line-search variants need at
  * least 10 line-search candidates, the pair variant at most 32). */
 #define MHPC_VARIANT_BWS 0            /* which: backward sweep */
-#define MHPC_VARIANT_BWS_1WAVE 1      /*   one wave per SIMD, no register cap */
-#define MHPC_VARIANT_BWS_2WAVE 2      /*   256-register build, two waves per SIMD */
-#define MHPC_VARIANT_BWS_PAIRWAVE 3   /*   two waves per problem (128-thread block, one per SIMD) */
+#define MHPC_VARIANT_BWS_ROWS4 1      /*   four problems per wave (one per 16-lane row) */
+#define MHPC_VARIANT_BWS_ROWS2 2      /*   two problems per wave (rows 0, 1) */
+#define MHPC_VARIANT_BWS_ROWS1 3      /*   one problem per wave (row 0) */
 #define MHPC_VARIANT_RO 1             /* which: line-search rollouts */
 #define MHPC_VARIANT_RO_PAIR 1        /*   two-wave pipeline, a lane pair per candidate */
 #define MHPC_VARIANT_RO_PIPE_STAGED 2 /*   two-wave pipeline, LDS-staged operands */

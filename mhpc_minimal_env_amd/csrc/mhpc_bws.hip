@@ -1,97 +1,57 @@
-// k_bws: the backward Riccati sweep of the batched HSDDP solve, one wavefront per problem.
+// k_bws: the backward Riccati sweep of the batched HSDDP solve, four problems per wavefront.
 //
 // Restates MultiPhaseDDP::backward_sweep + impact_aware_step (MultiPhaseDDP.cpp:100-127,
 // 300-341), SinglePhase::backward_sweep (SinglePhase.cpp:183-216), compute_Qfunction and
 // valuefunction_update (MHPC_CompoundTypes.h:117-144) and the regularisation retry loop of
 // MultiPhaseDDP::solve (:196-241).
 //
-// Per knot the 64 lanes share the dense blocks through LDS.  The dynamics Jacobian of a
-// planar model with state (q, qdot) and explicit Euler always has the shape
+// Layout (round 4).  A problem owns one 16-lane row of a wave (DPP row); its value function
+// and Q blocks live in registers, one matrix row per lane, and every product is a
+// row-broadcast multiply-add, v_fmac_f64_dpp row_newbcast:L (mhpc_dpp.h): the multiplicand
+// of lane L of the row reaches all 16 lanes inside the FMA, no LDS round trip.  The state
+// (NX = 2 NQ: 14 whole-body, 6 SRB) has at most 16 rows, so one row of lanes holds a whole
+// matrix.  Lane t of a row holds matrix row rho(t): the configuration rows q_i on the even
+// lanes 2i, the velocity rows NQ + i on the odd lanes 2i + 1, control rows on the lanes after
+// them (whole body: u0, u1 on lanes 14, 15, u2 / u3 as a second register set of lanes 14 / 15;
+// SRB: u0..u3 on lanes 6..9).
+//
+// The dynamics Jacobian of a planar model with state (q, qdot) and explicit Euler has the
+// shape
 //     [A B] = [ I  dt*I  0 ]      (rows 0..NQ-1, exact)
 //             [    W       ]      (rows NQ..NX-1: W = rows of I + dt*Ac | dt*Bc)
-// so every product with A or B is  a(col) * M[.., b(col)] + sum_r M[.., NQ+r] * W[r][col]
-// with a = 1 / dt / 0 and b = col / col-NQ.  Skipping the structural zeros of the dense
-// products of the reference changes no rounding (the skipped terms are exact zeros and the
-// remaining terms are summed in the same order).  C and D are non-zero only in the two
-// force rows of the stance foot (G2), and so is lyy.
+// so per knot, with H the value-function Hessian of knot k+1:
+//   S = H [A B]          S[i][c] = a(c) H[i][b(c)] + sum_r H[i][NQ+r] W[r][c]
+//                        (lane i: own H row, W[r][c] broadcast from the lane holding column c)
+//   Q = [A B]' S + ...   Q[c][d] = a(c) S[b(c)][d] + sum_r W[r][c] S[NQ+r][d]
+//                        (lane c: own W column, S[NQ+r][d] broadcast from lane 2r+1; the
+//                        a-term S[b(c)][d] of a velocity row is the configuration row on the
+//                        lane below: one quad_perm DPP move)
+// with a(c), b(c) = 1, c / dt, c - NQ / 0 for configuration / velocity / control columns.
+// C and D (stance rows of the contact forces) enter as rank-2 updates with broadcast rows.
+// Every lane of a row runs the same instruction stream; lanes that hold no matrix row compute
+// finite filler that no real row reads.
 //
-// Knot pipeline: the partials record of knot k-1 and its nominal state are loaded into
-// registers while knot k computes, and dropped into LDS at the top of the next knot.
+// The 4x4 control block is assembled on every lane (row broadcasts), tested for
+// positive-definiteness (unpivoted LDL^T, tests/test_psd_verdict.py) and inverted by 2x2
+// cofactors; Q is symmetric by construction in its control block and Qxx is symmetrised
+// through one LDS transpose per knot, as the reference does (MHPC_CompoundTypes.h:133-134).
+// The arithmetic is the reference's up to summation order (parity: tests/test_gpu_solve.py);
+// every launch shape (problems per wave) runs the same per-row code, so all of them agree bit
+// for bit (tests/test_gpu_variants.py).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "mhpc_device.h"
+#include "mhpc_dpp.h"
 
 namespace MHPC_NS {
 
-// Padded LDS shapes: every lane of a round runs the same straight-line code; rows / columns
-// past the real extents land in padding that no real output reads.
-// Sized for the 64- and the 128-thread block (see riccati_knot's static_asserts).
-constexpr int WS = 24;          // row stride of W / G2 (columns of [A B], padded)
-constexpr int JR = 24;          // rows of Jt (padded)
-constexpr int QR = 24;          // rows of Q (padded)
-// Row stride of Jt: NX + 1 puts the rows a half-wave reads together in R3 on distinct LDS
-// banks (stride NX = 14 doubles maps rows 16, 17 onto the banks of rows 0, 1).
-#ifndef MHPC_BWS_JTPAD
-#define MHPC_BWS_JTPAD 1
-#endif
-// Column-major blocks (MHPC_BWS_WT=1, default): the NQ dynamic rows of one column of [A B]
-// are contiguous in W (stride WR), the two stance rows of one column of [C D] in G2, and
-// the NQ entries Jt[row][NQ..NX-1] that R3 keeps in registers start 16-byte aligned (one
-// leading pad element per row), so R2 and R3 read their operand runs with ds_read_b128
-// (4 LDS cycles for 16 bytes per lane) instead of strided ds_read2_b64 pairs (8 cycles).
-// Jt row strides 18 / 10 doubles put the rows of a 16-lane b128 group on distinct banks
-// (tools/lds_bank_model_r3.py).  Only the LDS layout changes: same products, same order.
-#ifndef MHPC_BWS_WT
-#define MHPC_BWS_WT 1
-#endif
-#ifndef MHPC_BWS_WR
-#define MHPC_BWS_WR 8
-#endif
-// Row stride of the whole-body knot's H (the SRB knot's 6 x 6 H stays dense): 17 puts the
-// rows R45 stores and the column R2 reads on distinct banks (tools/lds_bank_model_r3.py)
-#ifndef MHPC_BWS_HS14
-#define MHPC_BWS_HS14 14
-#endif
-template <int NX> constexpr int HStride = NX == 14 ? MHPC_BWS_HS14 : NX;
-constexpr int WR = MHPC_BWS_WR;  // column stride of W (MHPC_BWS_WT)
-__device__ __forceinline__ constexpr int widx(int r, int col) {
-  return MHPC_BWS_WT ? col * WR + r : r * WS + col;
-}
-__device__ __forceinline__ constexpr int g2idx(int r, int col) {
-  return MHPC_BWS_WT ? col * 2 + r : r * WS + col;
-}
-template <int NX> constexpr int JtStride = MHPC_BWS_WT ? (NX == 14 ? 18 : 10) : NX + MHPC_BWS_JTPAD;
-constexpr int JtOff = MHPC_BWS_WT ? 1 : 0;
-// The NU = 4 control rows of Q ([Qux | Quu | Qu]) column-major in U (MHPC_BWS_UT=1, default):
-// R45 / R5 read a column of them (Qux[.][j], Qu) as two ds_read_b128 instead of four strided
-// reads.  uidx(c, k) = row NX + k, column c.
-#ifndef MHPC_BWS_UT
-#define MHPC_BWS_UT 1
-#endif
-// Row stride of Q for the WB knot and column stride of U: bank spreading of R3's stores and
-// R45's reads (tools/lds_bank_model_r3.py models every access of the whole-body knot: 575 ->
-// 543 LDS-array cycles at 31 / 10 against 22 / 4; measured at batch 4096, k_bws<64,2,2>
-// SQ_LDS_BANK_CONFLICT -18 %, SQ_LDS_IDX_ACTIVE -4.3 %, profiles/r03_bank_strides.txt)
-#ifndef MHPC_BWS_QS14
-#define MHPC_BWS_QS14 31
-#endif
-#ifndef MHPC_BWS_US
-#define MHPC_BWS_US 10
-#endif
-template <int NX> struct QShape {
-  static constexpr int NR = NX + 4;
-  static constexpr int QS = NX == 14 ? MHPC_BWS_QS14 : 13;  // row stride of Q; column QV holds Qv
-  static constexpr int QV = QS - 1;
-};
-
-// Arithmetic type of the 4x4 control block of a knot (adjugate, determinant, Quu^-1, the
-// gains tq = Qux' Quu^-1 and the products that update H / G / dV with them): the solve's
-// type, or double in the fp32 build (MHPC_BWS_WIDE, default; whole-body knots only): the fp32
-// sweep's gains then carry the rounding of the fp32 Q blocks only, not of an fp32 inversion
-// (C5 fp32: worst cost error vs the fp64 oracle 5.4e-3 -> 4.0e-3, gains after one sweep 3x
-// closer in the stance phases).
+// Arithmetic type of the whole-body knots' 4x4 control block (inverse, gains, and the H / G /
+// dV updates with them): the solve's type, or double in the fp32 build (MHPC_BWS_WIDE,
+// default): the fp32 sweep's gains then carry the rounding of the fp32 Q blocks only, not of
+// an fp32 inversion (tools/diag_fp32_stages.py).
 #ifndef MHPC_BWS_WIDE
 #define MHPC_BWS_WIDE 1
 #endif
@@ -101,196 +61,53 @@ using wreal = double;
 using wreal = real;
 #endif
 
-struct BwsLds {
-  alignas(16) real H[14 * MHPC_BWS_HS14];
-  alignas(16) real G[14];  // value function of knot k+1, then of knot k (row stride NX)
-  alignas(16) real W[MHPC_BWS_WT ? WS * WR : 7 * WS];  // rows NQ..NX-1 of [A B] (widx)
-  alignas(16) real G2[2 * WS];                         // stance rows of [C D] (g2idx)
-  real l[JR];          // (lx, lu)
-  real ldiag[18];      // diagonal running-cost Hessian (lxx, luu)
-  real lyy2[4], ly2[2];
-  union {
-    struct {
-      alignas(16) real Jt[JR * (MHPC_BWS_WT ? 18 : 15)];  // [A B]' H (NR x NX, JtStride<NX>)
-      real Q[QR * MHPC_BWS_QS14];  // Qxx (NX x NX), Qux (rows NX.., cols ..NX), Quu; column QV = Qv
-      alignas(16) real U[MHPC_BWS_QS14 * MHPC_BWS_US];  // rows NX..NX+3 of Q column-major (MHPC_BWS_UT)
-    };
-    struct {
-      real H2[196];      // impact-aware step: lifted H' and (Px' H2)
-      real Px[196];
-      real T[196];
-    };
-  };
-  real Qv[18];         // (Qx, Qu)
-  real xb[14], ub[4], yb[4], posk;  // nominal knot + its position reference
-  alignas(16) real Kst[56];          // results of the last knot, stored one knot later
-  alignas(16) wreal inv[16];         // Quu^-1 (unsymmetrised), broadcast through LDS
-  alignas(16) real dust[4];
-  real hx[14], Hs[9], G2v[14];
-  alignas(16) real junk[64];  // write target of the spare lanes of a round (never read)
-  acc dV;
-  int fail;
-#ifdef MHPC_BWS_TIMING
-  unsigned long long cyc[12], tlast;
-#endif
+template <int I>
+using ic = std::integral_constant<int, I>;
+template <int A, int B, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (A < B) {
+    f(ic<A>{});
+    sfor<A + 1, B>(f);
+  }
+}
+
+// Lane maps of one 16-lane row (see the file header).
+template <int NQ>
+struct Rows {
+  static constexpr int NX = 2 * NQ, NC = NX + 4;
+  // matrix row held by lane t (t >= NC: none; such lanes clamp their addresses)
+  static constexpr __host__ __device__ int rho(int t) {
+    return t < NX ? ((t & 1) ? NQ + (t >> 1) : (t >> 1)) : t;
+  }
+  // lane holding matrix row / column i (whole body: 16, 17 are the second set of 14, 15)
+  static constexpr __host__ __device__ int lam(int i) {
+    return i < NQ ? 2 * i : i < NX ? 2 * (i - NQ) + 1 : i < 16 ? i : 14 + (i - 16);
+  }
 };
 
-// Q entry (row NX + k, column c): in U (MHPC_BWS_UT) or in Q (row stride qs)
-__device__ __forceinline__ real& qu(BwsLds& sh, int qs, int nx, int k, int c) {
-  return MHPC_BWS_UT ? sh.U[c * MHPC_BWS_US + k] : sh.Q[(nx + k) * qs + c];
+// Value of lane K of this lane's 16-lane row.
+template <int K>
+__device__ __forceinline__ double rbc(double v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x150 + K, 0xf, 0xf, true);
 }
+template <int K>
+__device__ __forceinline__ float rbc(float v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x150 + K, 0xf, 0xf, true);
+}
+// quad_perm [0,0,2,2]: an odd lane takes the value of the even lane below it (the
+// configuration row matching a velocity row), an even lane keeps its own.
+__device__ __forceinline__ int qperm_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0xA0, 0xf, 0xf, true);
+}
+__device__ __forceinline__ double qperm(double v) {
+  return __hiloint2double(qperm_i(__double2hiint(v)), qperm_i(__double2loint(v)));
+}
+__device__ __forceinline__ float qperm(float v) { return __int_as_float(qperm_i(__float_as_int(v))); }
 
-// Optional cycle accounting per Riccati round (build with -DMHPC_BWS_TIMING; read with
-// mhpc_dbg_bws_cycles): slot i accumulates the cycles since the previous mark.
-#ifdef MHPC_BWS_TIMING
-#define BWS_TMARK(sh, lane, i)                          \
-  do {                                                  \
-    if ((lane) == 0) {                                  \
-      const unsigned long long t_ = clock64();          \
-      (sh).cyc[i] += t_ - (sh).tlast;                   \
-      (sh).tlast = t_;                                  \
-    }                                                   \
-  } while (0)
-__device__ unsigned long long g_bws_cyc[12];
-#else
-#define BWS_TMARK(sh, lane, i) do { } while (0)
-#endif
-
-// Eigen-style 4x4 inverse by cofactors (same formulas as the oracle).
-__device__ __forceinline__ void inverse4(const real* m, real* inv) {
-  real a[16];
-  a[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] +
-         m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
-  a[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] -
-         m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
-  a[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] +
-         m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
-  a[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] -
-          m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
-  a[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] -
-         m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
-  a[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] +
-         m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
-  a[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] -
-         m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
-  a[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] +
-          m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
-  a[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] +
-         m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
-  a[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] -
-         m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
-  a[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] +
-          m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
-  a[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] -
-          m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
-  a[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] -
-         m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
-  a[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] +
-         m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
-  a[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] -
-          m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
-  a[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] +
-          m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
-  const real det = m[0] * a[0] + m[1] * a[4] + m[2] * a[8] + m[3] * a[12];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) inv[i] = a[i] / det;
-}
-
-// Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209) on the lower triangle:
-// ldlt_inplace<Lower>::unblocked with diagonal pivoting (first largest |diagonal|), the
-// symmetric transposition applied to the lower triangle only, sign bookkeeping from
-// ZeroSign; true iff no strictly negative pivot.  Branch-free (the pivot swaps are
-// selects) so the scheduler can interleave it with the independent inverse / value-
-// function work of the same round; same arithmetic as the oracle.
-__device__ __forceinline__ void sel_swap(bool c, real& a, real& b) {
-  const real ta = a, tb = b;
-  a = c ? tb : ta;
-  b = c ? ta : tb;
-}
-__device__ __forceinline__ bool ldlt_is_positive4(real* A) {
-  int sign = 0;  // 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite
-  bool stop = false;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    int big = k;
-    real bv = fabs(A[k * 5]);
-#pragma unroll
-    for (int i = k + 1; i < 4; ++i) {
-      const real v = fabs(A[i * 5]);
-      const bool gt = v > bv;
-      bv = gt ? v : bv;
-      big = gt ? i : big;
-    }
-#pragma unroll
-    for (int I = k + 1; I < 4; ++I) {
-      const bool sw = big == I;
-#pragma unroll
-      for (int j = 0; j < k; ++j) sel_swap(sw, A[k * 4 + j], A[I * 4 + j]);
-#pragma unroll
-      for (int i = I + 1; i < 4; ++i) sel_swap(sw, A[i * 4 + k], A[i * 4 + I]);
-      sel_swap(sw, A[k * 5], A[I * 5]);
-#pragma unroll
-      for (int i = k + 1; i < I; ++i) sel_swap(sw, A[i * 4 + k], A[I * 4 + i]);
-    }
-    if (k > 0) {
-      real temp[3];
-#pragma unroll
-      for (int j = 0; j < k; ++j) temp[j] = A[j * 5] * A[k * 4 + j];
-      real s = 0;
-#pragma unroll
-      for (int j = 0; j < k; ++j) s += A[k * 4 + j] * temp[j];
-      A[k * 5] -= s;
-#pragma unroll
-      for (int i = k + 1; i < 4; ++i) {
-        real t = 0;
-#pragma unroll
-        for (int j = 0; j < k; ++j) t += A[i * 4 + j] * temp[j];
-        A[i * 4 + k] -= t;
-      }
-    }
-    const real akk = A[k * 5];
-    const bool valid = fabs(akk) > real(0.0);
-    if (k == 0) stop = !valid;  // whole diagonal zero: ZeroSign, stop
-#pragma unroll
-    for (int i = k + 1; i < 4; ++i) {
-      const real q = A[i * 4 + k] / akk;
-      A[i * 4 + k] = valid ? q : A[i * 4 + k];
-    }
-    int ns = sign;
-    if (sign == 1) ns = akk < real(0.0) ? 3 : 1;
-    else if (sign == 2) ns = akk > real(0.0) ? 3 : 2;
-    else if (sign == 0) ns = akk > real(0.0) ? 1 : (akk < real(0.0) ? 2 : 0);
-    sign = stop ? 0 : ns;
-  }
-  return sign == 1 || sign == 0;
-}
-
-// The verdict used by default (MHPC_BWS_PSD=1): an unpivoted LDL^T of the same matrix.
-// By Sylvester's law of inertia its pivots have the signs of the pivoted factorisation's
-// whenever no pivot is exactly zero, so the verdict is the same; a zero pivot leaves its
-// column, as in Eigen.  A quarter of the instructions of the pivoted test (no pivot search
-// or swaps, three reciprocals): -16 % backward-sweep time.  tests/test_psd_verdict.py
-// checks the agreement on PD, indefinite, rank-deficient and near-singular matrices;
-// MHPC_BWS_PSD=0 selects the pivoted restatement above.
-#ifndef MHPC_BWS_PSD
-#define MHPC_BWS_PSD 1
-#endif
-// MHPC_BWS_PSD_RCP (A/B): the pivots' reciprocals by the hardware estimate and two Newton
-// steps (<= 1 ulp) instead of IEEE divisions -- the verdict only reads signs.
-#ifndef MHPC_BWS_PSD_RCP
-#define MHPC_BWS_PSD_RCP 0
-#endif
-__device__ __forceinline__ real fast_recip(real a) {
-#if MHPC_BWS_PSD_RCP
-  real r = __builtin_amdgcn_rcp(a);
-  real e = fma(-a, r, real(1.0));
-  r = fma(r, e, r);
-  e = fma(-a, r, real(1.0));
-  return fma(r, e, r);
-#else
-  return real(1.0) / a;
-#endif
-}
+// Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209): an unpivoted LDL^T of
+// the lower triangle.  By Sylvester's law of inertia its pivots have the signs of Eigen's
+// pivoted factorisation's whenever no pivot is exactly zero, so the verdict is the same; a
+// zero pivot leaves its column, as in Eigen (tests/test_psd_verdict.py).
 __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
   bool neg = false;
 #pragma unroll
@@ -298,7 +115,7 @@ __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
     const real akk = A[k * 5];
     neg = neg || akk < real(0.0);
     const bool valid = akk != real(0.0);
-    const real r = fast_recip(valid ? akk : real(1.0));
+    const real r = real(1.0) / (valid ? akk : real(1.0));
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
       const real l = A[i * 4 + k] * r;
@@ -309,332 +126,309 @@ __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
   return !neg;
 }
 
-// Value of lane `src` (uniform) of a value held per lane: readlanes, no LDS.
-__device__ __forceinline__ float lane_bcast(float v, int src) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
-}
-__device__ __forceinline__ double lane_bcast(double v, int src) {
-  const long long b = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-// Row coefficient of the exact part of [A B] (see file header).
-template <int NQ>
-__device__ __forceinline__ real coef_a(int col, real dt) {
-  return col < NQ ? real(1.0) : (col < 2 * NQ ? dt : real(0.0));
-}
-template <int NQ>
-__device__ __forceinline__ int coef_b(int col) {
-  return col < NQ ? col : col - NQ;
-}
-
-// One Riccati knot.  On entry sh.{W,G2,l,lxx,luu,lyy2,ly2} hold the knot's derivatives and
-// sh.{H,G} the value function of knot k+1; on exit sh.{H,G} hold that of knot k.
-#ifndef MHPC_BWS_CH2
-#define MHPC_BWS_CH2 5
-#endif
-#ifndef MHPC_BWS_CH3
-#define MHPC_BWS_CH3 2
-#endif
-#ifndef MHPC_BWS_CH5
-#define MHPC_BWS_CH5 4
-#endif
-constexpr int CH2 = MHPC_BWS_CH2, CH3 = MHPC_BWS_CH3, CH5 = MHPC_BWS_CH5;
-#ifndef MHPC_BWS_INVLDS
-#define MHPC_BWS_INVLDS 1
-#endif
-
-// r2x / r45x: the caller's per-knot side work, run inside the R2 and R45 rounds (before
-// their barriers) so it needs no round of its own -- global traffic of the knot pipeline
-// (stores of the previous knot, prefetch of the next) and the drop of the next knot's
-// derivatives into LDS (nothing of R45 reads those arrays).
-template <int NT, int NQ, bool HAS_Y, class R2X, class R45X>
-__device__ bool riccati_knot(BwsLds& sh, int lane, real dt, real reg, real eps9, R2X&& r2x,
-                             R45X&& r45x) {
-  constexpr int NX = 2 * NQ, NR = NX + 4;
-  constexpr int QS = QShape<NX>::QS, QV = QShape<NX>::QV;
-  // the control block's arithmetic type: wreal for the whole-body knots (the fp32 sweep's
-  // gain errors come from them: tools/diag_fp32_stages.py), the solve's type for SRB knots
-  using wk = typename std::conditional<NQ == 7, wreal, real>::type;
-  // R2: Jt = [A B]' H (NR x NX) and Qv = (l + [A B]' G) + [C D]' ly, G taken as column NX
-  // of [H | G].  Lane = (column j, row group g): the column stays in registers and the lane
-  // runs T2 independent row chains.
-  {
-    constexpr int NC = NX + 1, GR = NT / NC, T2 = (NR + GR - 1) / GR;
-    static_assert(GR * T2 <= JR && GR * T2 <= QR && GR * T2 <= WS, "R2 padding");
-    const int j = lane % NC, g = lane / NC;
-    const bool isg = j == NX;
-    const bool wr = g < GR;                    // spare lanes write to the junk row
-    const real* col0 = isg ? sh.G : sh.H + j;  // [H | G] column j, element b at col0[b*cs]
-    real hc[NQ];
-#pragma unroll
-    for (int r = 0; r < NQ; ++r) hc[r] = col0[isg ? NQ + r : (NQ + r) * HStride<NX>];
-    real ly0 = real(0.0), ly1 = real(0.0);
-    if (HAS_Y) { ly0 = sh.ly2[0]; ly1 = sh.ly2[1]; }
-    // straight-line rows (no per-row branches, so the scheduler interleaves the T2 chains):
-    // the G-column extras are computed on every lane and selected
-    constexpr int C = T2 < CH2 ? T2 : CH2;
-#pragma unroll
-    for (int t0 = 0; t0 < T2; t0 += C) {
-      real acc[C];
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T2) continue;
-        const int row = g + GR * (t0 + u);  // < JR
-        const real a = coef_a<NQ>(row, dt);
-        const int bi = coef_b<NQ>(row);
-        const real hb = col0[isg ? bi : bi * HStride<NX>];
-        real sacc = a != real(0.0) ? a * hb : real(0.0);
-#pragma unroll
-        for (int r = 0; r < NQ; ++r) sacc += sh.W[widx(r, row)] * hc[r];
-        real tt = real(0.0);
-        if (HAS_Y) tt = sh.G2[g2idx(0, row)] * ly0 + sh.G2[g2idx(1, row)] * ly1;
-        const real gs = (sh.l[row] + sacc) + tt;
-        acc[u] = isg ? gs : sacc;
-      }
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T2) continue;
-        const int row = g + GR * (t0 + u);
-        real* dqv = &sh.Q[row * QS + QV];
-        if (MHPC_BWS_UT)  // Qu rows to U; padding rows (>= NR) to the junk slot
-          dqv = row < NX ? dqv : row < NR ? &sh.U[QV * MHPC_BWS_US + (row - NX)] : &sh.junk[lane & 63];
-        real* dst = isg ? dqv : &sh.Jt[row * JtStride<NX> + JtOff + j];
-        *(wr ? dst : &sh.junk[lane & 63]) = acc[u];
-      }
-    }
-  }
-  BWS_TMARK(sh, lane, NQ == 3 ? 4 : 3);
-  r2x();
-  __syncthreads();
-  BWS_TMARK(sh, lane, NQ == 3 ? 8 : 1);
-  // R3: Qxx = (lxx + C'lyy C) + A'HA ; Qux = (0 + D'lyy C) + B'HA ; Quu = (luu + D'lyy D) + B'HB
-  // (+ reg on the diagonal).  Lane = (row of Jt, column group g), the row Jt[row, NQ..] in
-  // registers, T3 independent column chains.
-  {
-    constexpr int RG = NT / NR, T3 = (NR + RG - 1) / RG;  // columns g + RG t < QV
-    static_assert(RG * T3 <= QV && RG * T3 <= WS, "R3 padding");
-    const int row = lane % NR, g = lane / NR;
-    const bool wr = g < RG;
-    real jr[NQ];
-#pragma unroll
-    for (int r = 0; r < NQ; ++r) jr[r] = sh.Jt[row * JtStride<NX> + JtOff + NQ + r];
-    real c0 = real(0.0), c1 = real(0.0);
-    if (HAS_Y) {
-      const real gr0 = sh.G2[g2idx(0, row)], gr1 = sh.G2[g2idx(1, row)];
-      c0 = gr0 * sh.lyy2[0] + gr1 * sh.lyy2[2];
-      c1 = gr0 * sh.lyy2[1] + gr1 * sh.lyy2[3];
-    }
-    const real dg = sh.ldiag[row];
-    constexpr int C = T3 < CH3 ? T3 : CH3;
-#pragma unroll
-    for (int t0 = 0; t0 < T3; t0 += C) {
-      real acc[C];
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T3) continue;
-        const int col = g + RG * (t0 + u);
-        const real a = coef_a<NQ>(col, dt);
-        const real jb = sh.Jt[row * JtStride<NX> + JtOff + coef_b<NQ>(col)];
-        real sacc = a != real(0.0) ? a * jb : real(0.0);
-#pragma unroll
-        for (int r = 0; r < NQ; ++r) sacc += jr[r] * sh.W[widx(r, col)];
-        const real base = row == col ? dg : real(0.0);
-        real e2 = real(0.0);
-        if (HAS_Y) e2 = c0 * sh.G2[g2idx(0, col)] + c1 * sh.G2[g2idx(1, col)];
-        real v = (base + e2) + sacc;
-        const real vr = v + real(1.0) * reg;
-        acc[u] = row == col ? vr : v;
-      }
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T3) continue;
-        const int col = g + RG * (t0 + u);
-        real* dq = MHPC_BWS_UT && row >= NX ? &sh.U[col * MHPC_BWS_US + (row - NX)] : &sh.Q[row * QS + col];
-        *(wr ? dq : &sh.junk[lane & 63]) = acc[u];
-      }
-    }
-  }
-  __syncthreads();
-  BWS_TMARK(sh, lane, NQ == 3 ? 9 : 2);
-  // R45: PSD test of Quu - 1e-9 I (every lane, registers, static indices); adjugate of Quu
-  // spread over lanes 0..15 (one 3x3 minor each) and broadcast back with readlane (no LDS
-  // round trip); then, in the same round, tq = Qux' Quu_inv, K = -tq', du, dV and
-  // H = sym(Qxx) - tq Qux, G = Qx - tq Qu.
-  wk q0[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) q0[c] = qu(sh, QS, NX, 0, NX + c);
-  wk adj = wk(0.0);
-  bool psd;
-  {
-    // the PSD verdict is applied at the end of the round: a failed knot abandons the sweep
-    // (everything written here is rewritten by the retry), only dV must stay untouched
-    const int i = (lane >> 2) & 3, j = lane & 3;  // lanes 0..15 of every wave
-    const int r0 = j == 0 ? 1 : 0, r1 = j <= 1 ? 2 : 1, r2 = j <= 2 ? 3 : 2;
-    const int c0 = i == 0 ? 1 : 0, c1 = i <= 1 ? 2 : 1, c2 = i <= 2 ? 3 : 2;
-#define QM(r, c) qu(sh, QS, NX, r, NX + (c))
-    const wk m00 = QM(r0, c0), m01 = QM(r0, c1), m02 = QM(r0, c2);
-    const wk m10 = QM(r1, c0), m11 = QM(r1, c1), m12 = QM(r1, c2);
-    const wk m20 = QM(r2, c0), m21 = QM(r2, c1), m22 = QM(r2, c2);
-#undef QM
-    real A[16];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        A[a * 4 + c] = qu(sh, QS, NX, a, NX + c) - (a == c ? real(1.0) * eps9 : real(0.0));
-#if MHPC_BWS_PSD == 1
-    psd = ldlt_nopiv_is_positive4(A);
-#elif MHPC_BWS_PSD == 2
-    psd = A[0] > -real(1e300);  // timing experiment only: no PSD test
-#else
-    psd = ldlt_is_positive4(A);
-#endif
-    // adj[i][j] = (-1)^(i+j) det(minor without row j, column i)
-    const wk det3 = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) +
-                         m02 * (m10 * m21 - m11 * m20);
-    adj = ((i + j) & 1) ? -det3 : det3;
-  }
-  const wk det = q0[0] * lane_bcast(adj, 0) + q0[1] * lane_bcast(adj, 4) +
-                      q0[2] * lane_bcast(adj, 8) + q0[3] * lane_bcast(adj, 12);
-  const wk invl = adj / det;
-  wk Qi[16];
-  {
-    wk inv[16];  // unsymmetrised inverse (uniform)
-#if MHPC_BWS_INVLDS
-    // through LDS: 16 readlane pairs would hold the inverse in 32 SGPRs, which the kernel's
-    // SGPR file cannot spare (it spills to VGPR lanes elsewhere in the knot loop)
-    // Lanes 0..15 store, every lane reads all 16 back, within one wave (NT == 64): the
-    // wave's LDS operations complete in issue order, and the compiler keeps the loads
-    // behind the store because they may alias it (same array, lane-dependent index).  Any
-    // explicit ordering costs: a wave barrier (a scheduling barrier) +9 % backward-sweep
-    // time, wavefront-scope fences +9 %, volatile accesses +28 % (MHPC_BWS_WAVEBAR = 1 / 3
-    // builds; A/B at batch 1024 in profiles/r02_ab_inverse_broadcast.txt).
-#ifndef MHPC_BWS_WAVEBAR
-#define MHPC_BWS_WAVEBAR 0
-#endif
-    // spare lanes: the junk slot (a two-slot one when wk is wider than real)
-    wreal* const jk = reinterpret_cast<wreal*>(
-        &sh.junk[std::is_same<wreal, real>::value ? (lane & 63) : (lane & 62)]);
-    *(lane < 16 ? &sh.inv[lane] : jk) = wreal(invl);
-    if (NT > 64) __syncthreads();
-#if MHPC_BWS_WAVEBAR == 1
-    else __builtin_amdgcn_wave_barrier();
-#elif MHPC_BWS_WAVEBAR == 3
-    else {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-#endif
-#pragma unroll
-    for (int e = 0; e < 16; ++e) inv[e] = sh.inv[e];
-#else
-#pragma unroll
-    for (int e = 0; e < 16; ++e) inv[e] = lane_bcast(invl, e);
-#endif
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) Qi[a * 4 + c] = (inv[a * 4 + c] + inv[c * 4 + a]) / 2;
-    // dV += -Qu' inv Qu, unsymmetrised inverse, no 1/2 (MHPC_CompoundTypes.h:142)
-    wk s = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      wk t = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t += qu(sh, QS, NX, k, QV) * inv[k * 4 + c];
-      s += t * qu(sh, QS, NX, c, QV);
-    }
-    // s and psd are uniform: every lane of wave 0 writes the same value (no divergent
-    // branch); the other waves of a 128-thread block must not re-read the updated dV
-    const acc dv0 = sh.dV;
-    acc* const jd = reinterpret_cast<acc*>(
-        &sh.junk[std::is_same<acc, real>::value ? (lane & 63) : (lane & 62)]);
-    *(lane < 64 ? &sh.dV : jd) = psd ? acc(dv0 + -s) : dv0;
-  }
-  {
-    // lane = (row i of [Qux | Qu]' , column group g); row NX stands for Qu (du), column NX
-    // of the update for G.  tq row i in registers; K[c][i] = -tq[i][c] exactly (Qi is
-    // symmetric and the sums run in the same order).
-    constexpr int NI = NX + 1, GC = NT / NI, T5 = (NX + 1 + GC - 1) / GC;
-    const int i = lane % NI, g = lane / NI;
-    const int si = i < NX ? i : QV;
-    wk qi[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) qi[k] = qu(sh, QS, NX, k, si);
-    wk tq[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      wk t = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t += qi[k] * Qi[k * 4 + c];
-      tq[c] = t;
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      *(g == 0 ? (i < NX ? &sh.Kst[c * NX + i] : &sh.dust[c]) : &sh.junk[lane & 63]) = real(-tq[c]);
-    constexpr int C = T5 < CH5 ? T5 : CH5;
-#pragma unroll
-    for (int t0 = 0; t0 < T5; t0 += C) {
-      real acc[C];
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T5) continue;
-        const int j = g + GC * (t0 + u);
-        const int sj = j < NX ? j : QV;
-        wk sacc = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) sacc += tq[c] * qu(sh, QS, NX, c, sj);
-        const real qij = sh.Q[i * QS + sj];
-        const real qji = sh.Q[(j < NX ? j : 0) * QS + i];
-        const real sym = (qij + qji) / 2;
-        const real base = j < NX ? sym : qij;
-        acc[u] = real(base - sacc);
-      }
-#pragma unroll
-      for (int u = 0; u < C; ++u) {
-        if (t0 + u >= T5) continue;
-        const int j = g + GC * (t0 + u);
-        const bool wr = g < GC && i < NX && j <= NX;
-        *(wr ? (j < NX ? &sh.H[i * HStride<NX> + j] : &sh.G[i]) : &sh.junk[lane & 63]) = acc[u];
-      }
-    }
-  }
-  BWS_TMARK(sh, lane, NQ == 3 ? 6 : 5);
-  r45x();
-  __syncthreads();
-  BWS_TMARK(sh, lane, NQ == 3 ? 10 : 7);
-  return psd;
+// Inverse of a symmetric 4x4 matrix by 2x2 cofactors (Laplace expansion along the first two
+// rows); the upper triangle is computed and mirrored, so the result is exactly symmetric --
+// the reference symmetrises Quu^-1 explicitly (MHPC_CompoundTypes.h:133).
+template <class T>
+__device__ __forceinline__ void inverse4_sym(const T (&m)[4][4], T (&v)[4][4]) {
+  const T s0 = m[0][0] * m[1][1] - m[1][0] * m[0][1];
+  const T s1 = m[0][0] * m[1][2] - m[1][0] * m[0][2];
+  const T s2 = m[0][0] * m[1][3] - m[1][0] * m[0][3];
+  const T s3 = m[0][1] * m[1][2] - m[1][1] * m[0][2];
+  const T s4 = m[0][1] * m[1][3] - m[1][1] * m[0][3];
+  const T s5 = m[0][2] * m[1][3] - m[1][2] * m[0][3];
+  const T c5 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
+  const T c4 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+  const T c3 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
+  const T c2 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+  const T c1 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
+  const T c0 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+  const T det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+  const T r = T(1.0) / det;
+  v[0][0] = (m[1][1] * c5 - m[1][2] * c4 + m[1][3] * c3) * r;
+  v[0][1] = (-m[0][1] * c5 + m[0][2] * c4 - m[0][3] * c3) * r;
+  v[0][2] = (m[3][1] * s5 - m[3][2] * s4 + m[3][3] * s3) * r;
+  v[0][3] = (-m[2][1] * s5 + m[2][2] * s4 - m[2][3] * s3) * r;
+  v[1][1] = (m[0][0] * c5 - m[0][2] * c2 + m[0][3] * c1) * r;
+  v[1][2] = (-m[3][0] * s5 + m[3][2] * s2 - m[3][3] * s1) * r;
+  v[1][3] = (m[2][0] * s5 - m[2][2] * s2 + m[2][3] * s1) * r;
+  v[2][2] = (m[3][0] * s4 - m[3][1] * s2 + m[3][3] * s0) * r;
+  v[2][3] = (-m[2][0] * s4 + m[2][1] * s2 - m[2][3] * s0) * r;
+  v[3][3] = (m[2][0] * s3 - m[2][1] * s1 + m[2][2] * s0) * r;
+  v[1][0] = v[0][1];
+  v[2][0] = v[0][2];
+  v[3][0] = v[0][3];
+  v[2][1] = v[1][2];
+  v[3][1] = v[1][3];
+  v[3][2] = v[2][3];
 }
 
-// Running-cost derivatives of a WB knot: lx / lxx per state lane (CostBase.cpp:28-31),
-// the control / force part comes precomputed with the partials record (see mhpc_solver.h).
-// The lane's weight and fixed reference are loaded once per phase (wb_cost_x_consts): a
-// lane-indexed __constant__ read inside the knot loop is a vector memory load whose wait
-// would also drain the knot's prefetch and stores.
-struct CostXConsts {
-  real w2;   // 2 dt Q[i]
-  real rx;   // reference of state i (unused for i = 0: the position reference)
+// Per-row LDS: the knot's Q rows for the Qxx transpose, and the value function at phase
+// boundaries (row-major by state index, pitch MP reals: 16-byte aligned rows).
+constexpr int MP = sizeof(real) == 8 ? 18 : 20;
+struct RowLds {
+  alignas(16) real M[16 * MP];
+  real Gs[16];
+  real hx[14], Hs[9], h;
 };
-__device__ __forceinline__ CostXConsts wb_cost_x_consts(int lane, const SolveParams& sp, int mode,
-                                                        real dt) {
-  CostXConsts c{real(0.0), real(0.0)};
-  if (lane < 14) {
-    const int i = lane;
-    c.rx = i == 1 ? sp.height : i == 2 ? real(0.0) : (i >= 3 && i < 7) ? cQjointBias[i - 3]
-           : i == 7 ? sp.vel : real(0.0);
-    c.w2 = 2 * dt * sp.cw.wQ[mode - 1][i];
-  }
-  return c;
+struct BwsLds {
+  RowLds r[4];
+};
+
+// What one lane knows about its row's problem.
+struct RowCtx {
+  int b;       // problem (clamped into the batch for a spare row)
+  int t;       // lane within the row
+  bool act;    // the row holds an active problem in this launch
+  bool live;   // the row takes part in the current sweep attempt
+  bool failed; // ... and its attempt has failed (PSD test) -- sticky for the attempt
+  int nom;     // nominal trajectory slot
+  real reg;    // regularisation of the attempt
+  acc dV;      // expected cost change (row-uniform)
+  int64_t kn, kn_wb, px_reads;
+};
+
+__device__ __forceinline__ bool go(const RowCtx& r) { return r.live && !r.failed; }
+__device__ __forceinline__ bool any_go(const RowCtx& r) {
+  return __builtin_amdgcn_ballot_w64(go(r)) != 0;
 }
-__device__ __forceinline__ void wb_cost_x(BwsLds& sh, int lane, const CostXConsts& c, real pos) {
-  if (lane < 14) {
-    const real rxi = lane == 0 ? pos : c.rx;
-    sh.l[lane] = c.w2 * (sh.xb[lane] - rxi);
-    sh.ldiag[lane] = c.w2;
+
+// ---------------------------------------------------------------------------------------
+// Whole-body phase (NQ = 7): knots N-2..0 from the value function in rl.M / rl.Gs (H, G of
+// knot N-1), result (knot 0) written back there.
+//
+// Per knot the partials record (mhpc_solver.h: 18 columns x (7 qddot rows + 2 force rows),
+// then lu, luu, ly, lyy) is read straight into the lanes that own its columns; the next
+// knot's record is loaded while the current one computes.
+template <bool STANCE>
+__device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+                         RowCtx& rc, int p) {
+  using R = Rows<7>;
+  using wk = wreal;
+  const int t = rc.t, b = rc.b;
+  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+  const real dt = sp.dt[p];
+  const int rho = R::rho(t);
+  const bool xl = t < 14;
+  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
+  // identity part of W: W[r][c] = dt * rec + (c == 7 + r)
+  real base[7];
+#pragma unroll
+  for (int r = 0; r < 7; ++r) base[r] = rho == 7 + r ? real(1.0) : real(0.0);
+  // running-cost weight and fixed reference of state rho (CostBase.cpp:28-31)
+  const int xi = xl ? rho : 0;
+  const real w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
+  const real rxc = xi == 1 ? sp.height : xi == 2 ? real(0.0)
+                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : real(0.0);
+  // lxx + reg on the diagonal of Qxx (Ixx * regularisation): added twice to the transposed
+  // copy in LDS, so that (Qxx + Qxx') / 2 carries it once
+  const real dg2 = xl ? 2 * (w2 + rc.reg) : real(0.0);
+  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
+  // prefetch registers (record of one knot): the lane's own column of [Ac Bc; C D], the
+  // second control column set (lanes 14, 15), one cost derivative per lane (broadcast below)
+  constexpr int NR = STANCE ? 9 : 7;  // rows of a record column read
+  constexpr int NCS = STANCE ? 14 : 8;  // cost derivatives (lu, luu [, ly, lyy])
+  real pr1[NR], pr2[NR], pcv, pxn, ppos;
+  const int c1 = rho;            // record column of W1 (0..15)
+  const int c2 = 16 + (t & 1);   // second set: control columns 2, 3 (lanes 14, 15)
+  const int cq = t < NCS ? t : 0;
+  auto load = [&](int k) {
+    const real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pr1[r] = rec[c1 * 9 + r];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pr2[r] = rec[c2 * 9 + r];
+    pcv = rec[PS_JAC + cq];
+    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    pxn = tk[xi];
+    ppos = pos[k];
+  };
+  real H[14], Gv;
+  {
+    const int hr = xl ? rho : 0;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) H[j] = rl.M[hr * MP + j];
+    Gv = rl.Gs[hr];
   }
+  const int cr = rho;  // column of M read in the transpose (Qxu columns for lanes 14, 15)
+  if (N >= 2) load(N - 2);
+  for (int k = N - 2; k >= 0; --k) {
+    // ---- the knot's derivatives (prefetched) ----
+    real W1[7], W2[7], G2o[2], G22[2];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) W1[r] = __builtin_fma(pr1[r], dt, base[r]);
+#pragma unroll
+    for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(pr2[r], dt, real(0.0));
+    G2o[0] = STANCE ? pr1[NR - 2] : real(0.0);
+    G2o[1] = STANCE ? pr1[NR - 1] : real(0.0);
+    G22[0] = STANCE ? pr2[NR - 2] : real(0.0);
+    G22[1] = STANCE ? pr2[NR - 1] : real(0.0);
+    // cost derivatives: lane q of the row holds entry q of (lu, luu, ly, lyy)
+    real luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
+    const real lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
+    luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
+    if (STANCE) {
+      ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
+      lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
+    }
+    const real rxi = rho == 0 ? ppos : rxc;
+    const real lx = w2 * (pxn - rxi);
+    const real l1 = xl ? lx : ((t & 1) ? lu1 : lu0);
+    const real l2 = (t & 1) ? lu3 : lu2;
+    const bool gate = go(rc);
+    rc.kn += gate ? 1 : 0;
+    rc.kn_wb += gate ? 1 : 0;
+    if (k > 0) load(k - 1);
+
+    // ---- S = H [A B] (lane: row rho of S) and Q = [A B]' S + ... (lane: row rho of Q),
+    // column block by column block (a Q column needs only its S column) ----
+    real S[18], Q[18], Q2[2], Qv1, Qv2;
+#pragma unroll
+    for (int c = 0; c < 7; ++c) S[c] = H[c];
+#pragma unroll
+    for (int c = 7; c < 14; ++c) S[c] = dt * H[c - 7];
+#pragma unroll
+    for (int c = 14; c < 18; ++c) S[c] = real(0.0);
+    real cc[2] = {0, 0}, cc2[2] = {0, 0};
+    if (STANCE) {
+      // C' lyy C etc.: cc[z] = sum_y G2[y][rho] lyy[y][z], then Q[.][d] += sum_z cc[z] G2[z][d]
+#pragma unroll
+      for (int z = 0; z < 2; ++z) {
+        cc[z] = G2o[0] * lyy[z] + G2o[1] * lyy[2 + z];
+        cc2[z] = G22[0] * lyy[z] + G22[1] * lyy[2 + z];
+      }
+    }
+#define MHPC_QINIT(c) Q[c] = coef * qperm(S[c])
+    dpp_sa7x4<0, 2, 4, 6>(S[0], S[1], S[2], S[3], W1, H + 7);
+    MHPC_QINIT(0); MHPC_QINIT(1); MHPC_QINIT(2); MHPC_QINIT(3);
+    dpp_sb_odd7_4(Q[0], Q[1], Q[2], Q[3], S[0], S[1], S[2], S[3], W1);
+    if (STANCE) dpp_sa2x4<0, 2, 4, 6>(Q[0], Q[1], Q[2], Q[3], G2o, cc);
+    dpp_sa7x4<8, 10, 12, 1>(S[4], S[5], S[6], S[7], W1, H + 7);
+    MHPC_QINIT(4); MHPC_QINIT(5); MHPC_QINIT(6); MHPC_QINIT(7);
+    dpp_sb_odd7_4(Q[4], Q[5], Q[6], Q[7], S[4], S[5], S[6], S[7], W1);
+    if (STANCE) dpp_sa2x4<8, 10, 12, 1>(Q[4], Q[5], Q[6], Q[7], G2o, cc);
+    dpp_sa7x4<3, 5, 7, 9>(S[8], S[9], S[10], S[11], W1, H + 7);
+    MHPC_QINIT(8); MHPC_QINIT(9); MHPC_QINIT(10); MHPC_QINIT(11);
+    dpp_sb_odd7_4(Q[8], Q[9], Q[10], Q[11], S[8], S[9], S[10], S[11], W1);
+    if (STANCE) dpp_sa2x4<3, 5, 7, 9>(Q[8], Q[9], Q[10], Q[11], G2o, cc);
+    dpp_sa7x4<11, 13, 14, 15>(S[12], S[13], S[14], S[15], W1, H + 7);
+    MHPC_QINIT(12); MHPC_QINIT(13); MHPC_QINIT(14); MHPC_QINIT(15);
+    dpp_sb_odd7_4(Q[12], Q[13], Q[14], Q[15], S[12], S[13], S[14], S[15], W1);
+    if (STANCE) dpp_sa2x4<11, 13, 14, 15>(Q[12], Q[13], Q[14], Q[15], G2o, cc);
+    dpp_sa7x2<14, 15>(S[16], S[17], W2, H + 7);
+    MHPC_QINIT(16); MHPC_QINIT(17);
+#undef MHPC_QINIT
+    Qv1 = __builtin_fma(coef, qperm(Gv), l1);
+    Q2[0] = real(0.0);
+    Q2[1] = real(0.0);
+    Qv2 = l2;
+    dpp_sb_odd7_3(Q[16], Q[17], Qv1, S[16], S[17], Gv, W1);
+    // control rows 2, 3 (second set of lanes 14, 15): only their control columns
+    dpp_sb_odd7_3(Q2[0], Q2[1], Qv2, S[16], S[17], Gv, W2);
+    if (STANCE) {
+      dpp_sa2x2<14, 15>(Q[16], Q[17], G22, cc);
+      dpp_sa2x2<14, 15>(Q2[0], Q2[1], G22, cc2);
+      Qv1 = (Qv1 + G2o[0] * ly[0]) + G2o[1] * ly[1];
+      Qv2 = (Qv2 + G22[0] * ly[0]) + G22[1] * ly[1];
+    }
+
+    // ---- Qxx transpose through LDS (symmetrisation, MHPC_CompoundTypes.h:134) ----
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rl.M[rho * MP + j] = Q[j];
+    {
+      real* dq = &rl.M[rho * MP + rho];
+      *dq = *dq + dg2;
+    }
+
+    // ---- the control block on every lane ----
+    wk q[4][4], Qu[4];
+    q[0][0] = rbc<14>(Q[14]); q[0][1] = rbc<14>(Q[15]); q[0][2] = rbc<14>(Q[16]); q[0][3] = rbc<14>(Q[17]);
+    q[1][1] = rbc<15>(Q[15]); q[1][2] = rbc<15>(Q[16]); q[1][3] = rbc<15>(Q[17]);
+    q[2][2] = rbc<14>(Q2[0]); q[2][3] = rbc<14>(Q2[1]); q[3][3] = rbc<15>(Q2[1]);
+    Qu[0] = rbc<14>(Qv1); Qu[1] = rbc<15>(Qv1); Qu[2] = rbc<14>(Qv2); Qu[3] = rbc<15>(Qv2);
+    // luu + reg on the diagonal (Iuu * regularisation)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[a][a] = q[a][a] + wk(luu[a] + rc.reg);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
+    bool psd;
+    {
+      real A[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) A[a * 4 + c] = real(q[a][c]) - (a == c ? sp.eps9 : real(0.0));
+      psd = ldlt_nopiv_is_positive4(A);
+    }
+    wk Qi[4][4];
+    inverse4_sym(q, Qi);
+    // du = -Quu^-1 Qu, dV += -Qu' Quu^-1 Qu (no 1/2, MHPC_CompoundTypes.h:137-142)
+    wk du[4], dv = wk(0.0);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      wk s = wk(0.0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qu[c];
+      du[a] = -s;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
+    // K = -Quu^-1 Qux: column rho on lane rho (Qux[m][rho] = Q[rho][14 + m], own)
+    wk Qxu[4], K[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) Qxu[m] = wk(Q[14 + m]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      wk s = wk(0.0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) s += Qi[a][m] * Qxu[m];
+      K[a] = -s;
+    }
+    // G = Qx - Qux' Quu^-1 Qu
+    wk Gn = wk(Qv1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
+    // H = sym(Qxx) - Qux' Quu^-1 Qux: H[rho][j] = Qs[j] + sum_a K[a] Qux[a][j]
+    wk Hn[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const real tj = rl.M[j * MP + cr];
+      Hn[j] = wk((Q[j] + tj) / 2);
+    }
+    dpp_sa4x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Qxu, K);
+    dpp_sa4x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Qxu, K);
+    dpp_sa4x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Qxu, K);
+    dpp_sa4x2<11, 13>(Hn[12], Hn[13], Qxu, K);
+#pragma unroll
+    for (int j = 0; j < 14; ++j) H[j] = real(Hn[j]);
+    Gv = real(Gn);
+    // ---- outputs of knot k (only while the row's attempt is alive) ----
+    const bool ok = gate && psd;
+    if (ok) {
+      const size_t rec = (size_t)b * sp.NK + ko + k;
+      if (xl) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = real(K[a]);
+        d.G[rec * 14 + rho] = real(Gn);
+      } else if (t == 14) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = real(du[a]);
+      }
+      rc.dV += acc(dv);
+    }
+    rc.failed = rc.failed || (gate && !psd);
+    if (!any_go(rc)) break;
+  }
+  // value function of knot 0 back to LDS
+  __syncthreads();
+  if (xl) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) rl.M[rho * MP + j] = H[j];
+    rl.Gs[rho] = Gv;
+  }
+  __syncthreads();
 }
 
 // SRB Jacobian entry of row 3+r, column col of [A B] (FBDynamics_par.c operation order).
@@ -661,493 +455,413 @@ __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const
   return bc * dt;
 }
 
-// Terminal value function of phase p (SinglePhase.cpp:189-191): G = Phix + Gnext,
-// H = Phixx + Hnext, with Gnext/Hnext in sh.G/sh.H; AL partials only while st->al_partials
-// (quirk B1: forward_sweep_partials_only does not add them).
-template <int NT, int NX>
-__device__ void terminal_value(const SolveParams& sp, const ProbState* st, BwsLds& sh, int lane,
-                               int p, real pos, const real* xe, real* Gout) {
+// ---------------------------------------------------------------------------------------
+// SRB phase (NQ = 3): the Jacobians are evaluated in registers (FBDynamics_par.c), the cost
+// derivatives from the nominal knot (CostBase.cpp:19-34).
+__device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+                          RowCtx& rc, int p) {
+  using R = Rows<3>;
+  const int t = rc.t, b = rc.b;
+  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+  const real dt = sp.dt[p];
+  const int rho = R::rho(t);
+  const bool xl = t < 6;
+  const int cj = rho < 10 ? rho : 0;  // column of [A B] held (clamped for spare lanes)
+  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
+  real foot[4], cs[2];
+  plan_foothold(traj_ptr(sp, d, b, rc.nom, ko), dt * N, mode, foot);
+  srb_contact(mode, cs);
+  const int m = mode - 1;
+  // per-lane cost weight 2 dt Q / 2 dt R and fixed reference of row cj
+  real w2, rxc;
+  if (cj < 6) {
+    w2 = 2 * dt * sp.cw.fQ[m][cj];
+    rxc = cj == 1 ? sp.height : cj == 3 ? sp.vel : real(0.0);
+  } else {
+    const int c = cj - 6;
+    w2 = 2 * dt * sp.cw.fR[m][c];
+    rxc = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
+  }
+  real luu[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) luu[c] = 2 * dt * sp.cw.fR[m][c];
+  const real dg2 = xl ? 2 * (w2 + rc.reg) : real(0.0);  // lxx + reg, see sweep_wb
+  // rows 3, 4 of W do not depend on the knot
+  const real zx[2] = {0, 0}, zu[4] = {0, 0, 0, 0};
+  const real W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
+  const real W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
+  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
+  real pxs[2], pus[4], pv, ppos;
+  auto load = [&](int k) {
+    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    pxs[0] = tk[0]; pxs[1] = tk[1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pus[c] = tk[6 + c];
+    pv = tk[cj];
+    ppos = pos[k];
+  };
+  real H[6], Gv;
+  {
+    const int hr = xl ? rho : 0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) H[j] = rl.M[hr * MP + j];
+    Gv = rl.Gs[hr];
+  }
+  const int cr = rho < 10 ? rho : 0;
+  if (N >= 2) load(N - 2);
+  for (int k = N - 2; k >= 0; --k) {
+    real W[3];
+    W[0] = W0c;
+    W[1] = W1c;
+    W[2] = srb_w_entry(2, cj, pxs, pus, foot, cs, dt);
+    const real rxi = rho == 0 ? ppos : rxc;
+    const real l1 = w2 * (pv - rxi);
+    const bool gate = go(rc);
+    rc.kn += gate ? 1 : 0;
+    if (k > 0) load(k - 1);
+    real S[10];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) S[c] = H[c];
+#pragma unroll
+    for (int c = 3; c < 6; ++c) S[c] = dt * H[c - 3];
+#pragma unroll
+    for (int c = 6; c < 10; ++c) S[c] = real(0.0);
+    dpp_sa3x4<0, 2, 4, 1>(S[0], S[1], S[2], S[3], W, H + 3);
+    dpp_sa3x4<3, 5, 6, 7>(S[4], S[5], S[6], S[7], W, H + 3);
+    dpp_sa3x2<8, 9>(S[8], S[9], W, H + 3);
+    real Q[10], Qv1;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) Q[c] = coef * qperm(S[c]);
+    Qv1 = __builtin_fma(coef, qperm(Gv), l1);
+    dpp_sb_odd3_4(Q[0], Q[1], Q[2], Q[3], S[0], S[1], S[2], S[3], W);
+    dpp_sb_odd3_4(Q[4], Q[5], Q[6], Q[7], S[4], S[5], S[6], S[7], W);
+    dpp_sb_odd3_3(Q[8], Q[9], Qv1, S[8], S[9], Gv, W);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) rl.M[(rho & 15) * MP + j] = Q[j];
+    {
+      real* dq = &rl.M[(rho & 15) * MP + (rho & 15)];
+      *dq = *dq + dg2;
+    }
+    real q[4][4], Qu[4];
+    q[0][0] = rbc<6>(Q[6]); q[0][1] = rbc<6>(Q[7]); q[0][2] = rbc<6>(Q[8]); q[0][3] = rbc<6>(Q[9]);
+    q[1][1] = rbc<7>(Q[7]); q[1][2] = rbc<7>(Q[8]); q[1][3] = rbc<7>(Q[9]);
+    q[2][2] = rbc<8>(Q[8]); q[2][3] = rbc<8>(Q[9]); q[3][3] = rbc<9>(Q[9]);
+    Qu[0] = rbc<6>(Qv1); Qu[1] = rbc<7>(Qv1); Qu[2] = rbc<8>(Qv1); Qu[3] = rbc<9>(Qv1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[a][a] = q[a][a] + (luu[a] + rc.reg);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
+    bool psd;
+    {
+      real A[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) A[a * 4 + c] = q[a][c] - (a == c ? sp.eps9 : real(0.0));
+      psd = ldlt_nopiv_is_positive4(A);
+    }
+    real Qi[4][4];
+    inverse4_sym(q, Qi);
+    real du[4], dv = real(0.0);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      real s = real(0.0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qu[c];
+      du[a] = -s;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
+    real Qxu[4], K[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Qxu[c] = Q[6 + c];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      real s = real(0.0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qxu[c];
+      K[a] = -s;
+    }
+    real Gn = Qv1;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
+    real Hn[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) Hn[j] = (Q[j] + rl.M[j * MP + cr]) / 2;
+    dpp_sa4x4<0, 2, 4, 1>(Hn[0], Hn[1], Hn[2], Hn[3], Qxu, K);
+    dpp_sa4x2<3, 5>(Hn[4], Hn[5], Qxu, K);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) H[j] = Hn[j];
+    Gv = Gn;
+    const bool ok = gate && psd;
+    if (ok) {
+      const size_t rec = (size_t)b * sp.NK + ko + k;
+      if (xl) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 6 + rho] = K[a];
+        d.G[rec * 14 + rho] = Gn;
+      } else if (t == 6) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = du[a];
+      }
+      rc.dV += acc(dv);
+    }
+    rc.failed = rc.failed || (gate && !psd);
+    if (!any_go(rc)) break;
+  }
+  __syncthreads();
+  if (xl) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) rl.M[rho * MP + j] = H[j];
+    rl.Gs[rho] = Gv;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------
+// Terminal value function of phase p (SinglePhase.cpp:189-191) in LDS: G = Phix + Gnext,
+// H = Phixx + Hnext; AL partials only while st->al_partials (quirk B1).  G of knot N-1 is
+// an output of the phase.
+template <int NX>
+__device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const ProbState* st,
+                               RowLds& rl, const RowCtx& rc, int p) {
   constexpr bool wb = NX == 14;
-  const int mode = sp.mode[p];
+  const int t = rc.t;
+  const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+  const real pos = d.refpos[(size_t)rc.b * sp.NK + ko + N - 1];
+  const real* xe = traj_ptr(sp, d, rc.b, rc.nom, ko + N - 1);
   const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
-  real h = 0;
-  if (al && lane == 0) {
-    real hx[14], Hs[3][3];
+  if (al && t == 0) {
+    real hx[14], Hs[3][3], h;
     if (mode == 2) wb_touchdown_compact<kFront>(xe, &h, hx, Hs);
     else wb_touchdown_compact<kBack>(xe, &h, hx, Hs);
 #pragma unroll
-    for (int i = 0; i < 14; ++i) sh.hx[i] = hx[i];
+    for (int i = 0; i < 14; ++i) rl.hx[i] = hx[i];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) sh.Hs[i] = Hs[i / 3][i % 3];
-    sh.G2v[0] = h;
+    for (int i = 0; i < 9; ++i) rl.Hs[i] = Hs[i / 3][i % 3];
+    rl.h = h;
   }
   __syncthreads();
-  if (al) h = sh.G2v[0];
+  const real h = al ? rl.h : real(0.0);
   const real s = st->sigma[p], lam = st->lambda[p];
   const int ih = mode == 2 ? 3 : 5;  // touchdown Hessian block (theta, hip, knee)
+  real* Gout = d.G + ((size_t)rc.b * sp.NK + ko + N - 1) * 14;
+  const bool gate = go(rc);
   #pragma unroll 1
-  for (int e = lane; e < NX * NX + NX; e += NT) {
+  for (int e = t; e < NX * NX + NX; e += 16) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
       real v = i == j ? (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) : real(0.0);
       if (al) {
         const int ai = i == 2 ? 0 : (i == ih ? 1 : (i == ih + 1 ? 2 : -1));
         const int aj = j == 2 ? 0 : (j == ih ? 1 : (j == ih + 1 ? 2 : -1));
-        const real hij = (ai >= 0 && aj >= 0) ? sh.Hs[ai * 3 + aj] : real(0.0);
-        v += 50 * (s * s / 2 * (sh.hx[i] * sh.hx[j] + h * hij) + lam * hij);
+        const real hij = (ai >= 0 && aj >= 0) ? rl.Hs[ai * 3 + aj] : real(0.0);
+        v += 50 * (s * s / 2 * (rl.hx[i] * rl.hx[j] + h * hij) + lam * hij);
       }
-      sh.H[i * HStride<NX> + j] = v + sh.H[i * HStride<NX> + j];
+      rl.M[i * MP + j] = v + rl.M[i * MP + j];
     } else {
       const int i = e - NX * NX;
       real rxi;
       if (wb) rxi = i == 0 ? pos : (i == 7 ? sp.vel : cXtermWB[mode - 1][i]);
       else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : real(0.0)));
       real v = (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) * (xe[i] - rxi);
-      if (al) v += 50 * (s * s / 2 * sh.hx[i] * h + lam * sh.hx[i]);
-      const real g = v + sh.G[i];
-      sh.G[i] = g;
-      Gout[i] = g;
+      if (al) v += 50 * (s * s / 2 * rl.hx[i] * h + lam * rl.hx[i]);
+      const real g = v + rl.Gs[i];
+      rl.Gs[i] = g;
+      if (gate) Gout[i] = g;
     }
   }
   __syncthreads();
 }
 
-// impact_aware_step (MultiPhaseDDP.cpp:300-341) for a WB phase p: sh.G/H hold CTG[0] of
-// phase p+1 (6-dim if that phase is SRB); on exit the 14-dim Gnext/Hnext of phase p.
-template <int NT>
-__device__ void impact_step(const SolveParams& sp, const DevBufs& d, int b, BwsLds& sh, int lane,
-                            int p, int64_t* px_reads) {
+// impact_aware_step (MultiPhaseDDP.cpp:300-341) for a WB phase p: rl.M / rl.Gs hold CTG[0] of
+// phase p+1 (6-dim if that phase is SRB); on exit the 14-dim Gnext / Hnext of phase p.
+__device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl, RowCtx& rc, int p) {
+  using R = Rows<7>;
+  const int t = rc.t;
   const int mode = sp.mode[p];
   const bool nwb = p + 1 < sp.n_wb;
   const bool imp = mode == 2 || mode == 4;
+  const int i = t < 14 ? R::rho(t) : 0;
   // lift to the full-model space: E' G', E' H' E (E = _stateProj for an SRB next phase)
-  #pragma unroll 1
-  for (int e = lane; e < 196 + 14; e += NT) {
-    if (e < 196) {
-      const int i = e / 14, j = e - i * 14;
-      real v;
-      if (nwb) v = sh.H[i * HStride<14> + j];
-      else {
-        const int pi = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
-        const int pj = j < 3 ? j : (j >= 7 && j < 10 ? j - 4 : -1);
-        v = (pi >= 0 && pj >= 0) ? sh.H[pi * 6 + pj] : real(0.0);
-      }
-      sh.H2[e] = v;
-    } else {
-      const int i = e - 196;
-      real v;
-      if (nwb) v = sh.G[i];
-      else {
-        const int q = i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1);
-        v = q >= 0 ? sh.G[q] : real(0.0);
-      }
-      sh.G2v[i] = v;
+  real H2[14], G2v;
+  {
+    const int pi = nwb ? i : (i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1));
+    const int pr = pi >= 0 ? pi : 0;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const int pj = nwb ? j : (j < 3 ? j : (j >= 7 && j < 10 ? j - 4 : -1));
+      const real v = pj >= 0 ? rl.M[pr * MP + pj] : real(0.0);
+      H2[j] = pi >= 0 ? v : real(0.0);
     }
+    G2v = pi >= 0 ? rl.Gs[pr] : real(0.0);
   }
+  real Hn[14], Gn;
   if (imp) {
-    const real* pxc = d.px + ((size_t)b * MAXP + p) * 196;  // column-major
-    #pragma unroll 1
-    for (int e = lane; e < 196; e += NT) sh.Px[(e % 14) * 14 + e / 14] = pxc[e];
-    if (lane == 0) ++*px_reads;
-  }
-  __syncthreads();
-  if (imp) {
-    // G = Px' G2 ; T = Px' H2 ; H = T Px
-    #pragma unroll 1
-    for (int e = lane; e < 196 + 14; e += NT) {
-      if (e < 196) {
-        const int i = e / 14, j = e - i * 14;
-        real s = 0;
+    // Px column i (column-major record): Pc[m] = Px[m][i]
+    const real* pxc = d.px + ((size_t)rc.b * MAXP + p) * 196 + i * 14;
+    real Pc[14];
 #pragma unroll
-        for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.H2[m * 14 + j];
-        sh.T[e] = s;
-      } else {
-        const int i = e - 196;
-        real s = 0;
+    for (int m = 0; m < 14; ++m) Pc[m] = pxc[m];
+    if (go(rc) && t == 0) ++rc.px_reads;
+    // T = Px' H2 (lane: row i), G = Px' G2: sum over m = 0..13 in order
+    real T[14];
 #pragma unroll
-        for (int m = 0; m < 14; ++m) s += sh.Px[m * 14 + i] * sh.G2v[m];
-        sh.G[i] = s;
-      }
-    }
-    __syncthreads();
-    #pragma unroll 1
-    for (int e = lane; e < 196; e += NT) {
-      const int i = e / 14, j = e - i * 14;
-      real s = 0;
+    for (int j = 0; j < 14; ++j) T[j] = real(0.0);
+    Gn = real(0.0);
+    dpp_sb_even7_4(T[0], T[1], T[2], T[3], H2[0], H2[1], H2[2], H2[3], Pc);
+    dpp_sb_even7_4(T[4], T[5], T[6], T[7], H2[4], H2[5], H2[6], H2[7], Pc);
+    dpp_sb_even7_4(T[8], T[9], T[10], T[11], H2[8], H2[9], H2[10], H2[11], Pc);
+    dpp_sb_even7_3(T[12], T[13], Gn, H2[12], H2[13], G2v, Pc);
+    dpp_sb_odd7_4(T[0], T[1], T[2], T[3], H2[0], H2[1], H2[2], H2[3], Pc + 7);
+    dpp_sb_odd7_4(T[4], T[5], T[6], T[7], H2[4], H2[5], H2[6], H2[7], Pc + 7);
+    dpp_sb_odd7_4(T[8], T[9], T[10], T[11], H2[8], H2[9], H2[10], H2[11], Pc + 7);
+    dpp_sb_odd7_3(T[12], T[13], Gn, H2[12], H2[13], G2v, Pc + 7);
+    // H = T Px: H[i][j] = sum_m T[i][m] Px[m][j], Px[m][j] on lane lam(j)
 #pragma unroll
-      for (int m = 0; m < 14; ++m) s += sh.T[i * 14 + m] * sh.Px[m * 14 + j];
-      sh.H[i * HStride<14> + j] = s;
-    }
+    for (int j = 0; j < 14; ++j) Hn[j] = real(0.0);
+    dpp_sa7x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Pc, T);
+    dpp_sa7x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Pc, T);
+    dpp_sa7x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Pc, T);
+    dpp_sa7x2<11, 13>(Hn[12], Hn[13], Pc, T);
+    dpp_sa7x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Pc + 7, T + 7);
+    dpp_sa7x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Pc + 7, T + 7);
+    dpp_sa7x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Pc + 7, T + 7);
+    dpp_sa7x2<11, 13>(Hn[12], Hn[13], Pc + 7, T + 7);
   } else {
-    #pragma unroll 1
-    for (int e = lane; e < 196; e += NT) sh.H[(e / 14) * HStride<14> + e % 14] = sh.H2[e];
-    if (lane < 14) sh.G[lane] = sh.G2v[lane];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) Hn[j] = H2[j];
+    Gn = G2v;
+  }
+  __syncthreads();
+  if (t < 14) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) rl.M[i * MP + j] = Hn[j];
+    rl.Gs[i] = Gn;
   }
   __syncthreads();
 }
 
-// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
-constexpr int kVmcnt0 = 0x0F70;
-
-#ifdef MHPC_FP32
-using real2 = float2;
-#else
-using real2 = double2;
-#endif
-// Store the staged K / du / G of knot record `rec`.  All global traffic of a knot (these
-// stores and the prefetch loads of the next record) is issued back to back right after the
-// wait for the previous prefetch, so the next wait (a full knot later) finds both retired:
-// gfx950 keeps one in-order VM counter for loads and stores.
-// Per-lane part of flush_knot, fixed for a phase: one 2-wide store per lane, one store
-// instruction per knot: K (2 NX pairs), du (2), G (NX / 2).  Lanes past them repeat lane 0's
-// store (same address, same value), so the store needs no divergent branch.
-struct FlushLane {
-  real* base;   // d.K / d.du / d.G
-  int stride;   // reals per knot record of that array
-  int o;        // pair offset (reals) inside the record
-  int src;      // staged source in the LDS block (reals from its start)
-};
-template <int NX>
-__device__ __forceinline__ FlushLane flush_lane(const DevBufs& d, const BwsLds& sh, int lane) {
-  constexpr int NK2 = 2 * NX, NG2 = NX / 2;
-  const int l = lane < NK2 + 2 + NG2 ? lane : 0;
-  const bool isk = l < NK2, isd = !isk && l < NK2 + 2;
-  FlushLane f;
-  f.o = 2 * (isk ? l : isd ? l - NK2 : l - NK2 - 2);
-  f.base = isk ? d.K : isd ? d.du : d.G;
-  f.stride = isk ? 56 : isd ? 4 : 14;
-  const real* src = isk ? sh.Kst : isd ? sh.dust : sh.G;
-  f.src = (int)(src - reinterpret_cast<const real*>(&sh)) + f.o;
-  return f;
-}
-template <int NT, int NX>
-__device__ __forceinline__ void flush_knot(size_t rec, const BwsLds& sh, const FlushLane& f) {
-#ifdef MHPC_BWS_NOSTORE
-  return;  // timing experiment only
-#endif
-  static_assert(2 * NX + 2 + NX / 2 <= NT, "flush lanes");
-  *reinterpret_cast<real2*>(f.base + rec * f.stride + f.o) =
-      *reinterpret_cast<const real2*>(reinterpret_cast<const real*>(&sh) + f.src);
-}
-
-// Backward sweep of one WB phase: knots N-2..0 with a one-knot register prefetch.
-// STANCE: a stance phase (modes 1, 3) carries the contact-force outputs y (C, D, ly, lyy);
-// one loop per variant keeps each variant's hoisted lane addresses out of the other's.
-template <int NT, bool STANCE>
-__device__ bool sweep_wb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
-                               BwsLds& sh, int lane, int p, real reg, int64_t* knots) {
-  const int N = sp.N[p], ko = sp.ko[p];
-  const real dt = sp.dt[p];
-  const int nom = st->nom_slot;
-  constexpr bool stance = STANCE;
-  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
-  // prefetch registers: PT doubles of the partials record + 1 of the nominal knot
-  constexpr int PT = (PS + NT - 1) / NT;
-  real pre[PT], prex = 0;
-  real* const shf = reinterpret_cast<real*>(&sh);
-  const int junk = (int)(sh.junk - shf) + (lane & 63);
-  const int xo = lane < 22 ? lane : 0;
-  const bool isref = lane == 22;
-  auto load = [&](int k) {
-    const real* prec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int e = lane + NT * t;
-      pre[t] = prec[e < PS ? e : PS - 1];  // unconditional: no exec-masked load
-    }
-    const real* tk = traj_ptr(sp, d, b, nom, ko + k);
-    prex = *(isref ? pos + k : tk + xo);
-  };
-  const CostXConsts cx = wb_cost_x_consts(lane, sp, sp.mode[p], dt);
-  // Where each prefetched record element goes, fixed for the phase: value = pre * mul + base
-  // into the LDS block at dst (W entries: (I + dt Ac | dt Bc), everything else verbatim:
-  // x * 1 + (-0) == x exactly); elements with no target write the lane's junk slot.
-  int dst[PT];
-  real mul[PT], base[PT];
-#pragma unroll
-  for (int t = 0; t < PT; ++t) {
-    const int e = lane + NT * t;
-    dst[t] = junk;
-    mul[t] = real(1.0);
-    base[t] = -real(0.0);
-    if (e < PS_JAC) {
-      const int col = e / 9, r = e - col * 9;
-      if (r < 7) {
-        dst[t] = (int)(sh.W - shf) + widx(r, col);
-        mul[t] = dt;
-        base[t] = col == 7 + r ? real(1.0) : real(0.0);
-      } else if (stance) {
-        dst[t] = (int)(sh.G2 - shf) + g2idx(r - 7, col);
-      }
-    } else if (e < PS) {
-      const int q = e - PS_JAC;  // lu 4, luu 4, ly 2, lyy 4
-      dst[t] = q < 4 ? (int)(sh.l - shf) + 14 + q
-             : q < 8 ? (int)(sh.ldiag - shf) + 14 + q - 4
-             : q < 10 ? (int)(sh.ly2 - shf) + q - 8 : (int)(sh.lyy2 - shf) + q - 10;
-    }
-  }
-  // lxx = 2 dt Q is constant over the phase (CostBase.cpp:28-31)
-  if (lane < 14) sh.ldiag[lane] = cx.w2;
-  const int dlx = lane < 14 ? (int)(sh.l - shf) + lane : junk;
-  // drop the prefetched knot into LDS: W = rows 7..13 of [I + dt Ac | dt Bc], G2 = [C D],
-  // the control / force cost derivatives, and lx from the nominal state in prex
-  // (CostBase.cpp:28-31; lane 22 holds the position reference)
-  auto drop = [&]() {
-    __builtin_amdgcn_s_waitcnt(kVmcnt0);  // the prefetch (and the stores issued before it)
-#pragma unroll
-    for (int t = 0; t < PT; ++t) shf[dst[t]] = __builtin_fma(pre[t], mul[t], base[t]);
-    const real pk = lane_bcast(prex, 22);
-    const real rxi = lane == 0 ? pk : cx.rx;
-    shf[dlx] = cx.w2 * (prex - rxi);
-  };
-  const FlushLane fl = flush_lane<14>(d, sh, lane);
-  load(N - 2);
-  drop();
-  __syncthreads();
-  for (int k = N - 2; k >= 0; --k) {
-    const int kk = ko + k;
-    auto r2x = [&]() {
-      if (k < N - 2) flush_knot<NT, 14>((size_t)b * sp.NK + kk + 1, sh, fl);
-      if (k > 0) load(k - 1);
-    };
-    auto r45x = [&]() {
-      if (k > 0) drop();
-    };
-    const bool ok = riccati_knot<NT, 7, STANCE>(sh, lane, dt, reg, sp.eps9, r2x, r45x);
-    ++*knots;
-    if (!ok) return false;
-  }
-  if (N >= 2) flush_knot<NT, 14>((size_t)b * sp.NK + ko, sh, fl);
-  return true;
-}
-
-template <int NT>
-__device__ bool sweep_fb_phase(const SolveParams& sp, const DevBufs& d, int b, const ProbState* st,
-                               BwsLds& sh, int lane, int p, real reg, int64_t* knots) {
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const real dt = sp.dt[p];
-  const int nom = st->nom_slot;
-  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
-  real foot[4], cs[2];
-  plan_foothold(traj_ptr(sp, d, b, nom, ko), dt * N, mode, foot);
-  srb_contact(mode, cs);
-  const int m = mode - 1;
-  // per-lane cost weight 2 dt Q (lanes 30..35: state i) / 2 dt R (lanes 36..39: control c)
-  // and fixed reference, hoisted out of the knot loop (see wb_cost_x_consts)
-  real fb_w2 = real(0.0), fb_rx = real(0.0);
-  if (lane >= 30 && lane < 36) {
-    const int i = lane - 30;
-    fb_w2 = 2 * dt * sp.cw.fQ[m][i];
-    fb_rx = i == 1 ? sp.height : i == 3 ? sp.vel : real(0.0);
-  } else if (lane >= 36 && lane < 40) {
-    const int c = lane - 36;
-    fb_w2 = 2 * dt * sp.cw.fR[m][c];
-    fb_rx = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
-  }
-  // every wave of the block loads the same nominal words (lane & 63), so the uniform W
-  // entries of the drop below are the same values whichever wave writes them
-  const int xo = (lane & 63) < 10 ? (lane & 63) : 0;
-  const bool isref = (lane & 63) == 10;
-  auto loadx = [&](int k) {  // unconditional single load per lane (no exec-masked load)
-    const real* tk = traj_ptr(sp, d, b, nom, ko + k);
-    return *(isref ? pos + k : tk + xo);
-  };
-  real* const shf = reinterpret_cast<real*>(&sh);
-  const int junk = (int)(sh.junk - shf) + (lane & 63);
-  // cost derivative slot of the lane (lanes 30..35: lx of state i, 36..39: lu of control c)
-  const int dl = lane >= 30 && lane < 40 ? (int)(sh.l - shf) + lane - 30 : junk;
-  const int shsrc = lane >= 30 && lane < 40 ? lane - 30 : 0;
-  // lxx / luu = 2 dt Q / 2 dt R are constant over the phase
-  if (lane >= 30 && lane < 40) sh.ldiag[lane - 30] = fb_w2;
-  // drop of knot k: the nominal (x 6, u 4) and position reference sit in prex of lanes
-  // 0..10; W rows (FBDynamics_par.c order) and the cost derivatives straight from registers.
-  // Only six entries of W (row 5: the torque terms) depend on the knot: they are uniform,
-  // so every lane computes and writes them; the rest is written once per phase (full).
-  auto drop = [&](real px, bool full) {
-    __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    const real xs[2] = {lane_bcast(px, 0), lane_bcast(px, 1)};
-    const real us[4] = {lane_bcast(px, 6), lane_bcast(px, 7), lane_bcast(px, 8),
-                          lane_bcast(px, 9)};
-    const real pk = lane_bcast(px, 10);
-    const real own = __shfl(px, shsrc);
-    if (full) {
-      if (lane < 30) {
-        const int r = lane / 10, col = lane - r * 10;
-        sh.W[widx(r, col)] = srb_w_entry(r, col, xs, us, foot, cs, dt);
-      }
-    } else {
-      sh.W[widx(2, 0)] = srb_w_entry(2, 0, xs, us, foot, cs, dt);
-      sh.W[widx(2, 1)] = srb_w_entry(2, 1, xs, us, foot, cs, dt);
-#pragma unroll
-      for (int c = 6; c < 10; ++c) sh.W[widx(2, c)] = srb_w_entry(2, c, xs, us, foot, cs, dt);
-    }
-    const real rxi = lane == 30 ? pk : fb_rx;
-    shf[dl] = fb_w2 * (own - rxi);
-  };
-  const FlushLane fl = flush_lane<6>(d, sh, lane);
-  real prex = loadx(N - 2);
-  drop(prex, true);
-  __syncthreads();
-  for (int k = N - 2; k >= 0; --k) {
-    const int kk = ko + k;
-    auto r2x = [&]() {
-      if (k < N - 2) flush_knot<NT, 6>((size_t)b * sp.NK + kk + 1, sh, fl);
-      if (k > 0) prex = loadx(k - 1);
-    };
-    auto r45x = [&]() {
-      if (k > 0) drop(prex, false);
-    };
-    const bool ok = riccati_knot<NT, 3, false>(sh, lane, dt, reg, sp.eps9, r2x, r45x);
-    ++*knots;
-    if (!ok) return false;
-  }
-  if (N >= 2) flush_knot<NT, 6>((size_t)b * sp.NK + ko, sh, fl);
-  return true;
-}
-
-// One sweep attempt with regularisation reg.  PART 0: every phase, from a zero terminal
-// value function (MultiPhaseDDP::backward_sweep).  PART 1: only the SRB phases (P-1 ..
-// n_wb), which read no partials record, so this launch can run beside the partials of the
-// same iteration.  PART 2: the WB phases (n_wb-1 .. 0), resuming from the value function
-// PART 1 left in d.carry.  PART 1 then PART 2 is PART 0's arithmetic, bit for bit (the
-// carried H / G / dV are stored and reloaded exactly).
-template <int NT, int PART>
-__device__ bool bws_sweep(const SolveParams& sp, const DevBufs& d, int b, ProbState* st, BwsLds& sh,
-                          real reg, int64_t* knots, int64_t* knots_wb, int64_t* px_reads,
-                          bool from_carry = true) {
-  const int lane = threadIdx.x;
-  const int nom = st->nom_slot;
-  if (PART == 2) {
-    // resume: the value function from d.carry, or as a PART 1 sweep of this kernel left it
-    const BwsCarry& c = d.carry[b];
-    if (from_carry) {
-      #pragma unroll 1
-      for (int e = lane; e < 196; e += NT) sh.H[e] = c.H[e];
-      if (lane < 14) sh.G[lane] = c.G[lane];
-    }
-  } else {
-    #pragma unroll 1
-    for (int e = lane; e < 14 * MHPC_BWS_HS14; e += NT) sh.H[e] = 0;  // Gnext = 0, Hnext = 0 (last phase)
-    if (lane < 14) sh.G[lane] = 0;
-    if (lane == 0) sh.dV = 0;
-  }
-  __syncthreads();
-  const int p_hi = PART == 2 ? sp.n_wb - 1 : sp.P - 1;
-  const int p_lo = PART == 1 ? sp.n_wb : 0;
+// One sweep attempt over phases p_hi..p_lo (MultiPhaseDDP::backward_sweep).  On entry
+// rl.M / rl.Gs hold the value function entering phase p_hi (zero for the last phase) and
+// rc.dV the matching dVnext.
+__device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState* st, RowLds& rl,
+                             RowCtx& rc, int p_hi, int p_lo) {
   for (int p = p_hi; p >= p_lo; --p) {
-    const bool wb = PART == 1 ? false : p < sp.n_wb;
-    const int N = sp.N[p], ko = sp.ko[p];
+    const bool wb = p < sp.n_wb;
+    const bool was_go = go(rc);
     if (p + 1 < sp.P) {
-      if constexpr (PART != 1) {
-        if (wb) impact_step<NT>(sp, d, b, sh, lane, p, px_reads);
-      }
-      if (lane == 0) sh.dV = st->dV[p + 1];  // dVnext
+      if (wb) impact_step(sp, d, rl, rc, p);
+      if (was_go) rc.dV = st->dV[p + 1];  // dVnext
     }
-    __syncthreads();
-    const real* pos = d.refpos + (size_t)b * sp.NK + ko;
-    real* Gp = d.G + ((size_t)b * sp.NK + ko + N - 1) * 14;
-    const real* xe = traj_ptr(sp, d, b, nom, ko + N - 1);
-    int64_t kn = 0;
-    bool ok;
-    if constexpr (PART != 1) {
-      if (wb) {
-        terminal_value<NT, 14>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
-        const int mode = sp.mode[p];
-        ok = (mode == 1 || mode == 3) ? sweep_wb_phase<NT, true>(sp, d, b, st, sh, lane, p, reg, &kn)
-                                      : sweep_wb_phase<NT, false>(sp, d, b, st, sh, lane, p, reg, &kn);
-        *knots_wb += kn;
-      }
+    if (wb) {
+      terminal_value<14>(sp, d, st, rl, rc, p);
+      const int mode = sp.mode[p];
+      if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
+      else sweep_wb<false>(sp, d, st, rl, rc, p);
+    } else {
+      terminal_value<6>(sp, d, st, rl, rc, p);
+      sweep_srb(sp, d, st, rl, rc, p);
     }
-    if (!wb) {
-      terminal_value<NT, 6>(sp, st, sh, lane, p, pos[N - 1], xe, Gp);
-      ok = sweep_fb_phase<NT>(sp, d, b, st, sh, lane, p, reg, &kn);
-    }
-    *knots += kn;
-    __syncthreads();
-    if (lane == 0) st->dV[p] = sh.dV;
-    __syncthreads();
-    if (!ok) return false;
+    if (was_go && rc.t == 0) st->dV[p] = rc.dV;
+    if (!any_go(rc)) break;
   }
-  return true;
 }
 
-// WAVES: minimum resident waves per SIMD requested from the register allocator.  One wave
-// per problem; while the batch fits one wave per SIMD (B <= 4 x CUs) the 1-wave build (no
-// register cap, widest ILP) is fastest, beyond that the 2-wave build hides latency by
-// co-residency.
+// Zero value function entering the last phase (MultiPhaseDDP.cpp:103-105).
+__device__ void zero_value(RowLds& rl, RowCtx& rc) {
+  __syncthreads();
+  #pragma unroll 1
+  for (int e = rc.t; e < 16 * MP; e += 16) rl.M[e] = real(0.0);
+  rl.Gs[rc.t] = real(0.0);
+  rc.dV = acc(0.0);
+  __syncthreads();
+}
+
+// RPW problems per wave (rows 0..RPW-1 of the wave; the others idle).
 //
 // PART 0: the whole sweep with its regularisation retries (MultiPhaseDDP.cpp:196-241).
 // PART 1: the SRB phases of the first attempt only, the value function at the WB boundary
-// saved to d.carry.  PART 2: the WB phases of the first attempt (if PART 1 passed), then the
-// same retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
-template <int NT, int WAVES, int PART>
-__global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, real update_reg) {
-  const int b = blockIdx.x;
-  if (b >= sp.B) return;
-  ProbState* st = &d.st[b];
-  if (!(st->active && st->ddp_active)) return;
+// saved to d.carry (this launch runs beside the partials, which it does not read).
+// PART 2: the WB phases of the first attempt (rows whose SRB part passed), then the same
+// retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
+template <int RPW, int PART>
+__global__ __launch_bounds__(64, 1) void k_bws(SolveParams sp, DevBufs d, real update_reg) {
   __shared__ BwsLds sh;
-  real reg = st->reg;
+  const int row = threadIdx.x >> 4;
+  RowCtx rc;
+  rc.t = threadIdx.x & 15;
+  const int b0 = blockIdx.x * RPW + row;
+  rc.b = b0 < sp.B ? b0 : sp.B - 1;
+  ProbState* st = &d.st[rc.b];
+  rc.act = row < RPW && b0 < sp.B && st->active && st->ddp_active;
+  if (!__builtin_amdgcn_ballot_w64(rc.act)) return;
+  RowLds& rl = sh.r[row];
+  rc.nom = st->nom_slot;
+  rc.reg = st->reg;
+  rc.kn = rc.kn_wb = rc.px_reads = 0;
+  rc.dV = acc(0.0);
   int bws_iter = 1;
-  int64_t knots = 0, knots_wb = 0, px_reads = 0, sweeps = 0;
+  int64_t sweeps = 0;
   bool aborted = false;
-  if constexpr (PART == 1) {
-    const bool ok = bws_sweep<NT, 1>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
-    BwsCarry& c = d.carry[b];
-    #pragma unroll 1
-    for (int e = threadIdx.x; e < 196; e += NT) c.H[e] = sh.H[e];
-    if (threadIdx.x < 14) c.G[threadIdx.x] = sh.G[threadIdx.x];
-    if (threadIdx.x == 0) {
-      c.ok = ok ? 1 : 0;
-      c.knots = (int32_t)knots;
+  bool pending = rc.act;
+  for (bool first = true;; first = false) {
+    rc.live = pending;
+    rc.failed = false;
+    sweeps += rc.live ? 1 : 0;
+    if (PART == 1) {
+      zero_value(rl, rc);
+      sweep_phases(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
+      BwsCarry& c = d.carry[rc.b];
+      __syncthreads();
+      if (rc.act) {
+        #pragma unroll 1
+        for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[(e / 6) * MP + e % 6];
+        if (rc.t < 6) c.G[rc.t] = rl.Gs[rc.t];
+        if (rc.t == 0) {
+          c.ok = rc.failed ? 0 : 1;
+          c.knots = (int32_t)rc.kn;
+        }
+      }
+      return;
     }
-    return;
-  }
-  if constexpr (PART == 2) {
-    // PART 0's loop below, the SRB half of its first attempt taken from PART 1; every
-    // retry runs both halves here (one call site each: the WB sweep code exists once)
-    const BwsCarry& c = d.carry[b];
-    knots = c.knots;
-    for (bool first = true;; first = false) {
-      ++sweeps;
-      bool ok = first ? c.ok != 0
-                      : bws_sweep<NT, 1>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads);
-      if (ok) ok = bws_sweep<NT, 2>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads, first);
-      if (ok) break;
-      reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
+    if (PART == 2 && first) {
+      // resume from the SRB half's value function (or retry if that half failed)
+      const BwsCarry& c = d.carry[rc.b];
+      __syncthreads();
+      #pragma unroll 1
+      for (int e = rc.t; e < 36; e += 16) rl.M[(e / 6) * MP + e % 6] = c.H[e];
+      if (rc.t < 6) rl.Gs[rc.t] = c.G[rc.t];
+      __syncthreads();
+      rc.failed = rc.live && c.ok == 0;
+      rc.kn += rc.live ? c.knots : 0;
+      rc.dV = st->dV[sp.n_wb];
+      sweep_phases(sp, d, st, rl, rc, sp.n_wb - 1, 0);
+    } else {
+      zero_value(rl, rc);
+      sweep_phases(sp, d, st, rl, rc, sp.P - 1, 0);
+    }
+    pending = rc.live && rc.failed;
+    if (pending) {
+      rc.reg = fmax(rc.reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
       ++bws_iter;
-      if (reg > 1000) { aborted = true; break; }
+      if (rc.reg > 1000) {
+        aborted = true;
+        pending = false;
+      }
     }
+    if (!__builtin_amdgcn_ballot_w64(pending)) break;
   }
-#ifdef MHPC_BWS_TIMING
-  if (threadIdx.x < 12) sh.cyc[threadIdx.x] = 0;
-  if (threadIdx.x == 0) sh.tlast = clock64();
-  const unsigned long long t_start = clock64();
-  __syncthreads();
-#endif
-  if constexpr (PART == 0) {
-    for (;;) {
-      ++sweeps;
-      if (bws_sweep<NT, 0>(sp, d, b, st, sh, reg, &knots, &knots_wb, &px_reads)) break;
-      reg = fmax(reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
-      ++bws_iter;
-      if (reg > 1000) { aborted = true; break; }
-    }
-  }
-  __syncthreads();
-#ifdef MHPC_BWS_TIMING
-  if (threadIdx.x == 0) sh.cyc[0] = clock64() - t_start;
-  __syncthreads();
-  if (threadIdx.x < 12) atomicAdd(&g_bws_cyc[threadIdx.x], sh.cyc[threadIdx.x]);
-#endif
-  if (threadIdx.x == 0) {
+  if (rc.act && rc.t == 0) {
     st->cnt[C_DDP]++;
     st->cnt[C_BWS] += sweeps;
-    st->cnt[C_BWS_KNOTS] += knots;
-    st->cnt[C_BWS_KNOTS_WB] += knots_wb;
-    st->cnt[C_BWS_KNOTS_FB] += knots - knots_wb;
-    st->cnt[C_PX_READS] += px_reads;
-    if (PART == 2) st->cnt[C_BWS_KNOTS_FB1] += d.carry[b].knots;
+    st->cnt[C_BWS_KNOTS] += rc.kn;
+    st->cnt[C_BWS_KNOTS_WB] += rc.kn_wb;
+    st->cnt[C_BWS_KNOTS_FB] += rc.kn - rc.kn_wb;
+    st->cnt[C_PX_READS] += rc.px_reads;
+    if (PART == 2) st->cnt[C_BWS_KNOTS_FB1] += d.carry[rc.b].knots;
     st->bws_iter = bws_iter;
     if (aborted) {  // "Regularization term exceeds maximum value": return from solve()
       st->status = MHPC_SOLVE_REG_ABORT;
@@ -1158,53 +872,32 @@ __global__ __launch_bounds__(NT, WAVES) void k_bws(SolveParams sp, DevBufs d, re
                                   (bws_iter & 0xff);
     } else {
       st->dV_exp = st->dV[0];  // _exp_cost_change = _phases[0]->_dV
-      reg = reg / 20;          // MultiPhaseDDP.cpp:237-241
+      real reg = rc.reg / 20;  // MultiPhaseDDP.cpp:237-241
       if (reg < real(1e-06)) reg = 0;
       st->reg = reg;
     }
   }
 }
 
-// Variant: sp.var_bws (mhpc_set_kernel_variant) or, by default by batch size on the
-// handle's device (sp.ncu CUs, 4 SIMDs each): two waves per problem (128-thread block, the
-// WB rounds' products split over twice the lanes: -20 % cycles per WB knot) while both fit
-// one SIMD each, the 1-wave build while one wave per problem does, the 2-wave (256-VGPR)
-// build beyond.  All builds compile the same source; tests/test_gpu_variants.py checks them
-// bit for bit.  The SRB half of a split sweep always runs 64-thread blocks (its rounds are
-// narrower than a wave).
-// part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).  The SRB half reads no
-// partials record and needs few registers (the WB code is not instantiated), so a partials
-// wave fits beside it on a SIMD.
-// Waves per SIMD the register allocator targets in the beyond-one-wave-per-SIMD build.
-#ifndef MHPC_BWS_MW
-#define MHPC_BWS_MW 2
-#endif
+// Launch shape: sp.var_bws (mhpc_set_kernel_variant) or, by default, four problems per wave
+// (one wave per block).  Two / one problems per wave run the same per-row code on fewer rows
+// (tests/test_gpu_variants.py checks them bit for bit).
+// part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, int part,
                       hipStream_t s) {
-#ifdef MHPC_BWS_WAVES
-  hipLaunchKernelGGL((k_bws<MHPC_BWS_NT, MHPC_BWS_WAVES, 0>), dim3(sp.B), dim3(MHPC_BWS_NT), 0, s,
-                     sp, d, update_reg);
-  (void)part;
-#else
-  const int v = sp.var_bws ? sp.var_bws
-                           : sp.B <= 2 * sp.ncu ? MHPC_VARIANT_BWS_PAIRWAVE
-                           : sp.B <= 4 * sp.ncu ? MHPC_VARIANT_BWS_1WAVE
-                                                : MHPC_VARIANT_BWS_2WAVE;
-  if (part == 1)
-    hipLaunchKernelGGL((k_bws<64, 2, 1>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else if (v == MHPC_VARIANT_BWS_PAIRWAVE && part == 2)
-    hipLaunchKernelGGL((k_bws<128, 1, 2>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
-  else if (v == MHPC_VARIANT_BWS_1WAVE && part == 2)
-    hipLaunchKernelGGL((k_bws<64, 1, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else if (v == MHPC_VARIANT_BWS_2WAVE && part == 2)
-    hipLaunchKernelGGL((k_bws<64, MHPC_BWS_MW, 2>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else if (v == MHPC_VARIANT_BWS_1WAVE)
-    hipLaunchKernelGGL((k_bws<64, 1, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else if (v == MHPC_VARIANT_BWS_2WAVE)
-    hipLaunchKernelGGL((k_bws<64, MHPC_BWS_MW, 0>), dim3(sp.B), dim3(64), 0, s, sp, d, update_reg);
-  else
-    hipLaunchKernelGGL((k_bws<128, 1, 0>), dim3(sp.B), dim3(128), 0, s, sp, d, update_reg);
-#endif
+  const int v = sp.var_bws ? sp.var_bws : MHPC_VARIANT_BWS_ROWS4;
+  const int rpw = v == MHPC_VARIANT_BWS_ROWS1 ? 1 : v == MHPC_VARIANT_BWS_ROWS2 ? 2 : 4;
+  const dim3 grid((sp.B + rpw - 1) / rpw);
+#define MHPC_LAUNCH_BWS(R)                                                                    \
+  do {                                                                                        \
+    if (part == 1) hipLaunchKernelGGL((k_bws<R, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    else if (part == 2) hipLaunchKernelGGL((k_bws<R, 2>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    else hipLaunchKernelGGL((k_bws<R, 0>), grid, dim3(64), 0, s, sp, d, update_reg);           \
+  } while (0)
+  if (rpw == 1) MHPC_LAUNCH_BWS(1);
+  else if (rpw == 2) MHPC_LAUNCH_BWS(2);
+  else MHPC_LAUNCH_BWS(4);
+#undef MHPC_LAUNCH_BWS
   return hipGetLastError();
 }
 
@@ -1215,17 +908,3 @@ bool bws_split(const SolveParams& sp) {
 }
 
 }  // namespace MHPC_NS
-
-#ifdef MHPC_BWS_TIMING
-extern "C" int mhpc_dbg_bws_cycles(unsigned long long* out, int reset) {
-  if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_bws_cyc), sizeof(unsigned long long) * 12) !=
-      hipSuccess)
-    return 1;
-  if (reset) {
-    unsigned long long z[12] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif

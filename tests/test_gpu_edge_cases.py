@@ -69,9 +69,9 @@ def test_edge_case_every_variant_bitwise(need_gpu, name):
     """The abort and the intermediate acceptances through the other launch variants."""
     desc, opt, x0 = E.inputs(name)
     base = run_gpu(desc, opt, x0)
-    for v in ({"bws": "2wave", "rollout": "fused", "overlap": "off"},
-              {"bws": "pairwave", "rollout": "pipe"},
-              {"bws": "1wave", "rollout": "fused_staged"}):
+    for v in ({"bws": "rows2", "rollout": "fused", "overlap": "off"},
+              {"bws": "rows1", "rollout": "pipe"},
+              {"bws": "rows4", "rollout": "fused_staged"}):
         got = run_gpu(desc, opt, x0, **v)
         for k in KEYS + ("trace", "status"):
             np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(base[k]), err_msg=f"{v} {k}")

@@ -61,11 +61,11 @@ def assert_oracle(got, ref, tol=SOLVE_TOL):
 
 
 ALL_VARIANTS = [(b, r, "auto") for b, r in
-                itertools.product(("1wave", "2wave", "pairwave"),
+                itertools.product(("rows4", "rows2", "rows1"),
                                   ("pair", "pipe_staged", "pipe", "fused_staged", "fused"))]
 # the backward sweep as one launch after the partials (the default splits it into an SRB
 # launch beside the partials and a WB launch after them)
-ALL_VARIANTS += [("1wave", "pair", "off"), ("2wave", "fused", "off"), ("pairwave", "pipe", "off"),
+ALL_VARIANTS += [("rows4", "pair", "off"), ("rows2", "fused", "off"), ("rows1", "pipe", "off"),
                  ("auto", "auto", "off")]
 
 
@@ -78,7 +78,7 @@ def test_variant_rejected_when_it_does_not_apply(need_gpu):
         for v in ("pair", "pipe_staged", "fused_staged"):
             with pytest.raises(RuntimeError):
                 loco.set_kernel_variant(rollout=v)
-        loco.set_kernel_variant(bws="2wave", rollout="fused")
+        loco.set_kernel_variant(bws="rows2", rollout="fused")
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 7, 0) == capi.MHPC_ERR_INVALID
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 2, 3) == capi.MHPC_ERR_INVALID
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 4) == capi.MHPC_ERR_INVALID
@@ -125,7 +125,7 @@ def test_sub_batches_bitwise(need_gpu, name, precision):
     base = solve(desc, x0, sub_batches=1)
     for n in (2, 3, 4):
         assert_bitwise(solve(desc, x0, sub_batches=n), base, f"{name}/{precision} {n} sub-batches")
-    assert_bitwise(solve(desc, x0, bws="1wave", rollout="fused", sub_batches=2), base,
+    assert_bitwise(solve(desc, x0, bws="rows4", rollout="fused", sub_batches=2), base,
                    f"{name}/{precision} 2 sub-batches, 1-wave sweep, fused line search")
     # batches barely larger than the block count: the even partition leaves no empty block
     for B in (5, 6):

@@ -1,9 +1,11 @@
-"""The build gate against the gfx950 register-allocator miscompile found in round 3
-(DESIGN.md §5): a live-range copy placed ahead of the EXEC restore of a divergent join block
-runs for no lane when the branch before it was skipped.  The checker must flag that shape,
-pass the legal placements, and pass every kernel TU of the shipping build.  The same gate pins
-the order of the sweep's barrier-free inverse broadcast (round-2 review, weak 5): the 16 LDS
-reads of the inverse must follow the lane-0..15 store in every k_bws kernel."""
+"""The build gates on device assembly (csrc/Makefile, _build/isa.ok):
+  * the gfx950 register-allocator miscompile found in round 3: a live-range copy
+    placed ahead of the EXEC restore of a divergent join block runs for no lane when the branch
+    before it was skipped -- the checker must flag that shape and pass the legal placements;
+  * DPP read-after-write hazards (round 4): the sweep's row-broadcast multiply-adds are inline
+    assembly (mhpc_dpp.h), outside the compiler's hazard recognizer; a DPP instruction may not
+    read a VGPR written in the previous 2 wait states.
+Both must pass every kernel TU of the shipping build."""
 import os
 import subprocess
 import sys
@@ -13,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import check_exec_prologue as C  # noqa: E402
-import check_inv_broadcast as I  # noqa: E402
+import check_dpp_hazards as D  # noqa: E402
 
 CSRC = os.path.join(ROOT, "mhpc_minimal_env_amd", "csrc")
 
@@ -23,12 +25,45 @@ def test_checker_flags_the_miscompile_shape_only():
     assert [(h[0], h[1], h[3]) for h in hits] == [("bad_kernel", ".LBB0_4", [168, 169])]
 
 
-def test_inverse_broadcast_checker_flags_hoisted_reads():
-    """tests/golden/isa_inv_broadcast.s: one site as the shipping build emits it and two copies
-    with one / all of the window's reads moved above the store."""
-    sites, bad = I.scan(os.path.join(ROOT, "tests", "golden", "isa_inv_broadcast.s"))
-    assert sites == {"_ZN4mhpc5k_bwsILi64ELi2ELi1EEEvgood": 1}
-    assert sorted(b[0].rsplit("Ev", 1)[1] for b in bad) == ["all_reads_hoisted", "one_read_hoisted"]
+def test_dpp_hazard_checker(tmp_path):
+    """A DPP read of a VGPR written 1 wait state earlier (source or accumulator) is flagged;
+    2 wait states (s_nop 1, or two instructions) pass; a v_fmac_*_dpp right after a label
+    (unknown predecessor) is flagged unless an s_nop covers it."""
+    f = "row_newbcast:1 row_mask:0xf bank_mask:0xf"
+    src = "\n".join([
+        "good:",
+        "\ts_nop 1",
+        "\tv_mul_f64 v[2:3], v[0:1], v[0:1]",
+        "\ts_nop 1",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        f"\tv_fmac_f64_dpp v[8:9], v[2:3], v[6:7] {f}",
+        f"\tv_fmac_f64_dpp v[10:11], v[2:3], v[6:7] {f}",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        "src_hazard:",
+        "\ts_nop 1",
+        "\tv_mul_f64 v[2:3], v[0:1], v[0:1]",
+        "\ts_nop 0",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        "acc_hazard:",
+        "\ts_nop 1",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        f"\tv_fmac_f64_dpp v[8:9], v[2:3], v[6:7] {f}",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        "label_hazard:",
+        f"\tv_fmac_f64_dpp v[4:5], v[2:3], v[6:7] {f}",
+        ""])
+    p = tmp_path / "h.s"
+    p.write_text(src)
+    bad = D.check(str(p))
+    assert sorted(b.split(": ")[1] for b in bad) == ["acc_hazard", "label_hazard", "src_hazard"]
+
+
+def test_generated_dpp_header_is_current():
+    """mhpc_dpp.h is what tools/gen_dpp_asm.py generates."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_dpp_asm.py")],
+                       capture_output=True, text=True, check=True)
+    with open(os.path.join(CSRC, "mhpc_dpp.h")) as f:
+        assert f.read() == r.stdout
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
@@ -38,7 +73,7 @@ def test_shipping_kernels_have_no_misplaced_join_copy():
     isa = [os.path.join(CSRC, "_build", f) for f in ("kernels.s", "bws.s", "kernels32.s", "bws32.s")]
     assert C.scan_all(isa) == []
     sweeps = [os.path.join(CSRC, "_build", f) for f in ("bws.s", "bws32.s")]
-    assert I.main(sweeps) == 0
-    for p in sweeps:  # two knot kinds (or one) in each of the seven k_bws instantiations
-        sites, _ = I.scan(p)
-        assert len(sites) == 7 and all(n >= 1 for n in sites.values()), sites
+    assert D.main(sweeps) == 0
+    for p in sweeps:  # the row-broadcast FMAs are there (the gate checked something)
+        with open(p) as f:
+            assert f.read().count("_dpp ") > 1000
