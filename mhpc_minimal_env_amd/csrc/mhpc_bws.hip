@@ -104,6 +104,21 @@ __device__ __forceinline__ double qperm(double v) {
 }
 __device__ __forceinline__ float qperm(float v) { return __int_as_float(qperm_i(__float_as_int(v))); }
 
+// 1 / a by the hardware estimate and two Newton steps (within an ulp of the division; the
+// IEEE division sequence is twice the instructions and latency)
+__device__ __forceinline__ double recip(double a) {
+  double r = __builtin_amdgcn_rcp(a);
+  double e = __builtin_fma(-a, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-a, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ float recip(float a) {
+  float r = __builtin_amdgcn_rcpf(a);
+  const float e = __builtin_fmaf(-a, r, 1.0f);
+  return __builtin_fmaf(r, e, r);
+}
+
 // Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209): an unpivoted LDL^T of
 // the lower triangle.  By Sylvester's law of inertia its pivots have the signs of Eigen's
 // pivoted factorisation's whenever no pivot is exactly zero, so the verdict is the same; a
@@ -114,13 +129,13 @@ __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
   for (int k = 0; k < 4; ++k) {
     const real akk = A[k * 5];
     neg = neg || akk < real(0.0);
-    const bool valid = akk != real(0.0);
-    const real r = real(1.0) / (valid ? akk : real(1.0));
+    // a zero pivot leaves its column (r = 0: the updates subtract exact zeros)
+    const real r = akk != real(0.0) ? recip(akk) : real(0.0);
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
       const real l = A[i * 4 + k] * r;
 #pragma unroll
-      for (int j = k + 1; j <= i; ++j) A[i * 4 + j] -= valid ? l * A[j * 4 + k] : real(0.0);
+      for (int j = k + 1; j <= i; ++j) A[i * 4 + j] -= l * A[j * 4 + k];
     }
   }
   return !neg;
@@ -144,7 +159,7 @@ __device__ __forceinline__ void inverse4_sym(const T (&m)[4][4], T (&v)[4][4]) {
   const T c1 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
   const T c0 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
   const T det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
-  const T r = T(1.0) / det;
+  const T r = recip(det);
   v[0][0] = (m[1][1] * c5 - m[1][2] * c4 + m[1][3] * c3) * r;
   v[0][1] = (-m[0][1] * c5 + m[0][2] * c4 - m[0][3] * c3) * r;
   v[0][2] = (m[3][1] * s5 - m[3][2] * s4 + m[3][3] * s3) * r;
@@ -278,6 +293,15 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     rc.kn_wb += gate ? 1 : 0;
+    // everything derived from the prefetch registers before they are reloaded: the loads
+    // (memory operations) stay behind these volatile statements, so the buffers of knot k
+    // and k - 1 share registers (no copy of a loop-carried buffer at the back edge)
+    asm volatile("" ::"v"(W1[0]), "v"(W1[1]), "v"(W1[2]), "v"(W1[3]), "v"(W1[4]), "v"(W1[5]),
+                 "v"(W1[6]), "v"(W2[0]), "v"(W2[1]), "v"(W2[2]), "v"(W2[3]), "v"(W2[4]),
+                 "v"(W2[5]), "v"(W2[6]), "v"(l1), "v"(l2));
+    asm volatile("" ::"v"(G2o[0]), "v"(G2o[1]), "v"(G22[0]), "v"(G22[1]), "v"(luu[0]),
+                 "v"(luu[1]), "v"(luu[2]), "v"(luu[3]), "v"(ly[0]), "v"(ly[1]), "v"(lyy[0]),
+                 "v"(lyy[1]), "v"(lyy[2]), "v"(lyy[3]));
     if (k > 0) load(k - 1);
 
     // ---- S = H [A B] (lane: row rho of S) and Q = [A B]' S + ... (lane: row rho of Q),
@@ -298,36 +322,33 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
         cc2[z] = G22[0] * lyy[z] + G22[1] * lyy[2 + z];
       }
     }
-#define MHPC_QINIT(c) Q[c] = coef * qperm(S[c])
-    dpp_sa7x4<0, 2, 4, 6>(S[0], S[1], S[2], S[3], W1, H + 7);
-    MHPC_QINIT(0); MHPC_QINIT(1); MHPC_QINIT(2); MHPC_QINIT(3);
-    dpp_sb_odd7_4(Q[0], Q[1], Q[2], Q[3], S[0], S[1], S[2], S[3], W1);
-    if (STANCE) dpp_sa2x4<0, 2, 4, 6>(Q[0], Q[1], Q[2], Q[3], G2o, cc);
-    dpp_sa7x4<8, 10, 12, 1>(S[4], S[5], S[6], S[7], W1, H + 7);
-    MHPC_QINIT(4); MHPC_QINIT(5); MHPC_QINIT(6); MHPC_QINIT(7);
-    dpp_sb_odd7_4(Q[4], Q[5], Q[6], Q[7], S[4], S[5], S[6], S[7], W1);
-    if (STANCE) dpp_sa2x4<8, 10, 12, 1>(Q[4], Q[5], Q[6], Q[7], G2o, cc);
-    dpp_sa7x4<3, 5, 7, 9>(S[8], S[9], S[10], S[11], W1, H + 7);
-    MHPC_QINIT(8); MHPC_QINIT(9); MHPC_QINIT(10); MHPC_QINIT(11);
-    dpp_sb_odd7_4(Q[8], Q[9], Q[10], Q[11], S[8], S[9], S[10], S[11], W1);
-    if (STANCE) dpp_sa2x4<3, 5, 7, 9>(Q[8], Q[9], Q[10], Q[11], G2o, cc);
-    dpp_sa7x4<11, 13, 14, 15>(S[12], S[13], S[14], S[15], W1, H + 7);
-    MHPC_QINIT(12); MHPC_QINIT(13); MHPC_QINIT(14); MHPC_QINIT(15);
-    dpp_sb_odd7_4(Q[12], Q[13], Q[14], Q[15], S[12], S[13], S[14], S[15], W1);
-    if (STANCE) dpp_sa2x4<11, 13, 14, 15>(Q[12], Q[13], Q[14], Q[15], G2o, cc);
-    dpp_sa7x2<14, 15>(S[16], S[17], W2, H + 7);
-    MHPC_QINIT(16); MHPC_QINIT(17);
-#undef MHPC_QINIT
+    // column blocks 0..5, 6..11, 12..17: S block, then the Q block it feeds
+    wb_s_a(S[0], S[1], S[2], S[3], S[4], S[5], W1, W2, H + 7);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) Q[c] = coef * qperm(S[c]);
+    sb_odd7_6(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], S + 0, W1);
+    if (STANCE) wb_st_a(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], G2o, cc);
+    wb_s_b(S[6], S[7], S[8], S[9], S[10], S[11], W1, W2, H + 7);
+#pragma unroll
+    for (int c = 6; c < 12; ++c) Q[c] = coef * qperm(S[c]);
+    sb_odd7_6(Q[6], Q[7], Q[8], Q[9], Q[10], Q[11], S + 6, W1);
+    if (STANCE) wb_st_b(Q[6], Q[7], Q[8], Q[9], Q[10], Q[11], G2o, cc);
+    wb_s_c(S[12], S[13], S[14], S[15], S[16], S[17], W1, W2, H + 7);
+#pragma unroll
+    for (int c = 12; c < 18; ++c) Q[c] = coef * qperm(S[c]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
     Q2[0] = real(0.0);
     Q2[1] = real(0.0);
     Qv2 = l2;
-    dpp_sb_odd7_3(Q[16], Q[17], Qv1, S[16], S[17], Gv, W1);
-    // control rows 2, 3 (second set of lanes 14, 15): only their control columns
-    dpp_sb_odd7_3(Q2[0], Q2[1], Qv2, S[16], S[17], Gv, W2);
+    {
+      const real sc[7] = {S[12], S[13], S[14], S[15], S[16], S[17], Gv};
+      sb_odd7_7(Q[12], Q[13], Q[14], Q[15], Q[16], Q[17], Qv1, sc, W1);
+      // control rows 2, 3 (second set of lanes 14, 15): only their control columns
+      const real s2[3] = {S[16], S[17], Gv};
+      sb_odd7_3(Q2[0], Q2[1], Qv2, s2, W2);
+    }
     if (STANCE) {
-      dpp_sa2x2<14, 15>(Q[16], Q[17], G22, cc);
-      dpp_sa2x2<14, 15>(Q2[0], Q2[1], G22, cc2);
+      wb_st_c(Q[12], Q[13], Q[14], Q[15], Q[16], Q[17], Q2[0], Q2[1], G2o, G22, cc, cc2);
       Qv1 = (Qv1 + G2o[0] * ly[0]) + G2o[1] * ly[1];
       Qv2 = (Qv2 + G22[0] * ly[0]) + G22[1] * ly[1];
     }
@@ -397,10 +418,8 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
       const real tj = rl.M[j * MP + cr];
       Hn[j] = wk((Q[j] + tj) / 2);
     }
-    dpp_sa4x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Qxu, K);
-    dpp_sa4x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Qxu, K);
-    dpp_sa4x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Qxu, K);
-    dpp_sa4x2<11, 13>(Hn[12], Hn[13], Qxu, K);
+    wb_h_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Qxu, K);
+    wb_h_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Qxu, K);
 #pragma unroll
     for (int j = 0; j < 14; ++j) H[j] = real(Hn[j]);
     Gv = real(Gn);
@@ -518,6 +537,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     const real l1 = w2 * (pv - rxi);
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
+    asm volatile("" ::"v"(W[2]), "v"(l1));  // see sweep_wb
     if (k > 0) load(k - 1);
     real S[10];
 #pragma unroll
@@ -526,16 +546,19 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     for (int c = 3; c < 6; ++c) S[c] = dt * H[c - 3];
 #pragma unroll
     for (int c = 6; c < 10; ++c) S[c] = real(0.0);
-    dpp_sa3x4<0, 2, 4, 1>(S[0], S[1], S[2], S[3], W, H + 3);
-    dpp_sa3x4<3, 5, 6, 7>(S[4], S[5], S[6], S[7], W, H + 3);
-    dpp_sa3x2<8, 9>(S[8], S[9], W, H + 3);
+    srb_s_a(S[0], S[1], S[2], S[3], S[4], W, H + 3);
     real Q[10], Qv1;
 #pragma unroll
-    for (int c = 0; c < 10; ++c) Q[c] = coef * qperm(S[c]);
+    for (int c = 0; c < 5; ++c) Q[c] = coef * qperm(S[c]);
+    sb_odd3_5(Q[0], Q[1], Q[2], Q[3], Q[4], S + 0, W);
+    srb_s_b(S[5], S[6], S[7], S[8], S[9], W, H + 3);
+#pragma unroll
+    for (int c = 5; c < 10; ++c) Q[c] = coef * qperm(S[c]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
-    dpp_sb_odd3_4(Q[0], Q[1], Q[2], Q[3], S[0], S[1], S[2], S[3], W);
-    dpp_sb_odd3_4(Q[4], Q[5], Q[6], Q[7], S[4], S[5], S[6], S[7], W);
-    dpp_sb_odd3_3(Q[8], Q[9], Qv1, S[8], S[9], Gv, W);
+    {
+      const real sc[6] = {S[5], S[6], S[7], S[8], S[9], Gv};
+      sb_odd3_6(Q[5], Q[6], Q[7], Q[8], Q[9], Qv1, sc, W);
+    }
 #pragma unroll
     for (int j = 0; j < 10; ++j) rl.M[(rho & 15) * MP + j] = Q[j];
     {
@@ -590,8 +613,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     real Hn[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) Hn[j] = (Q[j] + rl.M[j * MP + cr]) / 2;
-    dpp_sa4x4<0, 2, 4, 1>(Hn[0], Hn[1], Hn[2], Hn[3], Qxu, K);
-    dpp_sa4x2<3, 5>(Hn[4], Hn[5], Qxu, K);
+    srb_h(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Qxu, K);
 #pragma unroll
     for (int j = 0; j < 6; ++j) H[j] = Hn[j];
     Gv = Gn;
@@ -711,25 +733,20 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl,
 #pragma unroll
     for (int j = 0; j < 14; ++j) T[j] = real(0.0);
     Gn = real(0.0);
-    dpp_sb_even7_4(T[0], T[1], T[2], T[3], H2[0], H2[1], H2[2], H2[3], Pc);
-    dpp_sb_even7_4(T[4], T[5], T[6], T[7], H2[4], H2[5], H2[6], H2[7], Pc);
-    dpp_sb_even7_4(T[8], T[9], T[10], T[11], H2[8], H2[9], H2[10], H2[11], Pc);
-    dpp_sb_even7_3(T[12], T[13], Gn, H2[12], H2[13], G2v, Pc);
-    dpp_sb_odd7_4(T[0], T[1], T[2], T[3], H2[0], H2[1], H2[2], H2[3], Pc + 7);
-    dpp_sb_odd7_4(T[4], T[5], T[6], T[7], H2[4], H2[5], H2[6], H2[7], Pc + 7);
-    dpp_sb_odd7_4(T[8], T[9], T[10], T[11], H2[8], H2[9], H2[10], H2[11], Pc + 7);
-    dpp_sb_odd7_3(T[12], T[13], Gn, H2[12], H2[13], G2v, Pc + 7);
+    {
+      const real h2b[8] = {H2[7], H2[8], H2[9], H2[10], H2[11], H2[12], H2[13], G2v};
+      sb_even7_7(T[0], T[1], T[2], T[3], T[4], T[5], T[6], H2, Pc);
+      sb_even7_8(T[7], T[8], T[9], T[10], T[11], T[12], T[13], Gn, h2b, Pc);
+      sb_odd7_7(T[0], T[1], T[2], T[3], T[4], T[5], T[6], H2, Pc + 7);
+      sb_odd7_8(T[7], T[8], T[9], T[10], T[11], T[12], T[13], Gn, h2b, Pc + 7);
+    }
     // H = T Px: H[i][j] = sum_m T[i][m] Px[m][j], Px[m][j] on lane lam(j)
 #pragma unroll
     for (int j = 0; j < 14; ++j) Hn[j] = real(0.0);
-    dpp_sa7x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Pc, T);
-    dpp_sa7x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Pc, T);
-    dpp_sa7x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Pc, T);
-    dpp_sa7x2<11, 13>(Hn[12], Hn[13], Pc, T);
-    dpp_sa7x4<0, 2, 4, 6>(Hn[0], Hn[1], Hn[2], Hn[3], Pc + 7, T + 7);
-    dpp_sa7x4<8, 10, 12, 1>(Hn[4], Hn[5], Hn[6], Hn[7], Pc + 7, T + 7);
-    dpp_sa7x4<3, 5, 7, 9>(Hn[8], Hn[9], Hn[10], Hn[11], Pc + 7, T + 7);
-    dpp_sa7x2<11, 13>(Hn[12], Hn[13], Pc + 7, T + 7);
+    wb_p_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Pc, T);
+    wb_p_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Pc, T);
+    wb_p_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Pc + 7, T + 7);
+    wb_p_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Pc + 7, T + 7);
   } else {
 #pragma unroll
     for (int j = 0; j < 14; ++j) Hn[j] = H2[j];
@@ -747,20 +764,27 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl,
 // One sweep attempt over phases p_hi..p_lo (MultiPhaseDDP::backward_sweep).  On entry
 // rl.M / rl.Gs hold the value function entering phase p_hi (zero for the last phase) and
 // rc.dV the matching dVnext.
+// WB_CODE = false: SRB phases only (the SRB half of a split sweep), no whole-body code in the
+// kernel (its register allocation is the SRB knot's, so a partials wave fits beside it).
+template <bool WB_CODE>
 __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState* st, RowLds& rl,
                              RowCtx& rc, int p_hi, int p_lo) {
   for (int p = p_hi; p >= p_lo; --p) {
-    const bool wb = p < sp.n_wb;
+    const bool wb = WB_CODE && p < sp.n_wb;
     const bool was_go = go(rc);
     if (p + 1 < sp.P) {
-      if (wb) impact_step(sp, d, rl, rc, p);
+      if constexpr (WB_CODE) {
+        if (wb) impact_step(sp, d, rl, rc, p);
+      }
       if (was_go) rc.dV = st->dV[p + 1];  // dVnext
     }
     if (wb) {
-      terminal_value<14>(sp, d, st, rl, rc, p);
-      const int mode = sp.mode[p];
-      if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
-      else sweep_wb<false>(sp, d, st, rl, rc, p);
+      if constexpr (WB_CODE) {
+        terminal_value<14>(sp, d, st, rl, rc, p);
+        const int mode = sp.mode[p];
+        if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
+        else sweep_wb<false>(sp, d, st, rl, rc, p);
+      }
     } else {
       terminal_value<6>(sp, d, st, rl, rc, p);
       sweep_srb(sp, d, st, rl, rc, p);
@@ -813,7 +837,7 @@ __global__ __launch_bounds__(64, 1) void k_bws(SolveParams sp, DevBufs d, real u
     sweeps += rc.live ? 1 : 0;
     if (PART == 1) {
       zero_value(rl, rc);
-      sweep_phases(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
+      sweep_phases<false>(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
       BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       if (rc.act) {
@@ -838,10 +862,10 @@ __global__ __launch_bounds__(64, 1) void k_bws(SolveParams sp, DevBufs d, real u
       rc.failed = rc.live && c.ok == 0;
       rc.kn += rc.live ? c.knots : 0;
       rc.dV = st->dV[sp.n_wb];
-      sweep_phases(sp, d, st, rl, rc, sp.n_wb - 1, 0);
+      sweep_phases<true>(sp, d, st, rl, rc, sp.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
-      sweep_phases(sp, d, st, rl, rc, sp.P - 1, 0);
+      sweep_phases<true>(sp, d, st, rl, rc, sp.P - 1, 0);
     }
     pending = rc.live && rc.failed;
     if (pending) {

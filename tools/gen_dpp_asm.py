@@ -7,90 +7,144 @@ row_newbcast (gfx950: DPP on a 64-bit VALU op supports row_newbcast only).
 One instruction per broadcast multiply-add; the compiler emits v_mov_b64_dpp + v_fmac for
 the same source (it does not fold DPP into a 64-bit FMA), twice the issue slots.
 
+A block is a list of accumulators and, per round, one term per accumulator; the rounds are
+issued round robin over the accumulators (so one accumulator's chain is spaced by the
+block's width: a gfx950 FP64 FMA takes ~2 issue slots of dependent latency, and wide blocks
+issue at full rate, tools/ubench/dpp_rate.hip).
+
 Hazard rule (GCNHazardRecognizer::checkDPPHazards, MI300 ISA "manually inserted wait
 states"): a DPP instruction may not read a VGPR written in the previous 2 wait states.  The
-compiler cannot see inside inline assembly, so every block here
+compiler cannot see inside inline assembly, so every block
   * starts with s_nop 1 (2 wait states: covers whatever the compiler placed before it), and
-  * cycles its accumulators round robin; a block with fewer than 3 accumulators pads with
-    s_nop so that an accumulator is never re-read within 2 wait states of its last write.
-Sources and multipliers are never written inside a block.  tools/check_dpp_hazards.py checks
-the shipped assembly for the rule (build gate, csrc/Makefile).
-
-Shapes (T = float or double; lanes as template constants or literal lists):
-  sa<R,C>:   acc[c] += sum_r bcast(s[r], L_c) * m[r]      (one broadcast lane per column)
-  sb_<list>: acc[c] += sum_r bcast(s_c, list[r]) * m[r]   (one broadcast source per column)
+  * pads with s_nop when it has fewer than 3 accumulators, so that an accumulator is never
+    re-read within 2 wait states of its last write.
+Sources and multipliers are never written inside a block.  The blocks are volatile: they keep
+their source order (the sweep interleaves S and Q column blocks to bound register pressure).
+tools/check_dpp_hazards.py checks the shipped assembly for the rule (build gate,
+csrc/Makefile).
 
 usage: python tools/gen_dpp_asm.py > mhpc_minimal_env_amd/csrc/mhpc_dpp.h
 """
 
-LISTS = {
-    "odd7": [1, 3, 5, 7, 9, 11, 13],
-    "even7": [0, 2, 4, 6, 8, 10, 12],
-    "odd3": [1, 3, 5],
-}
-SA = [(r, c) for r in (2, 3, 4, 7) for c in (1, 2, 3, 4)]
-SB = [(name, c) for name in LISTS for c in (1, 2, 3, 4)]
+
+def lam(nq, i):
+    """Lane of matrix row / column i in a 16-lane row (mhpc_bws.hip: Rows<NQ>::lam)."""
+    nx = 2 * nq
+    if i < nq:
+        return 2 * i
+    if i < nx:
+        return 2 * (i - nq) + 1
+    return i if i < 16 else 14 + (i - 16)
 
 
-def body(ins, nacc, mnem):
-    """Instruction lines; ins = list of (acc index, src operand, m operand, lane text)."""
-    lines = ["s_nop 1"]
-    # round robin over the accumulators: instruction i reads/writes acc i % nacc; with fewer
-    # than 3 accumulators the same accumulator would come back within 2 wait states
-    pad = max(0, 3 - nacc)
-    for k, (a, s, m, lane) in enumerate(ins):
-        if k and pad and k % nacc == 0:
-            lines.append(f"s_nop {pad - 1}")
-        lines.append(f"{mnem} %{a}, %{s}, %{m} row_newbcast:{lane} row_mask:0xf bank_mask:0xf")
-    return "\\n\\t".join(lines)
+class Block:
+    """terms[r][a] = (src operand text, m operand text, lane) for accumulator a in round r."""
+
+    def __init__(self, name, naccs, arrays, terms, doc):
+        self.name, self.naccs, self.arrays, self.terms, self.doc = name, naccs, arrays, terms, doc
+
+    def emit(self):
+        # operand numbering: accumulators, then every array element used (in order of use)
+        ops, index = [], {}
+        nxt = self.naccs
+        for rnd in self.terms:
+            for src, m, _ in rnd:
+                for e in (src, m):
+                    if e not in index:
+                        index[e] = nxt
+                        ops.append(e)
+                        nxt += 1
+        assert nxt <= 30, (self.name, nxt)
+        out = [f"// {self.doc}",
+               "template <class T>",
+               f"__device__ __forceinline__ void {self.name}("
+               + ", ".join(f"T& a{a}" for a in range(self.naccs)) + ", "
+               + ", ".join(f"const T* {n}" for n in self.arrays) + ") {"]
+        for t, mn in (("double", "v_fmac_f64_dpp"), ("float", "v_fmac_f32_dpp")):
+            lines = ["s_nop 1"]
+            pad = max(0, 3 - self.naccs)
+            k = 0
+            for rnd in self.terms:
+                for a, (src, m, lane) in enumerate(rnd):
+                    if k and pad and k % self.naccs == 0:
+                        lines.append(f"s_nop {pad - 1}")
+                    lines.append(f"{mn} %{a}, %{index[src]}, %{index[m]} row_newbcast:{lane} "
+                                 "row_mask:0xf bank_mask:0xf")
+                    k += 1
+            kw = "if constexpr (sizeof(T) == 8)" if t == "double" else "else"
+            out.append(f"  {kw}")
+            out.append('    asm volatile("' + "\\n\\t".join(lines) + '"')
+            out.append("        : " + ", ".join(f'"+v"(a{a})' for a in range(self.naccs)))
+            out.append("        : " + ", ".join(f'"v"({e})' for e in ops) + ");")
+        out.append("}")
+        return "\n".join(out)
 
 
-def gen_sa(r, c):
-    # operands: acc 0..c-1, s c..c+r-1, m c+r..c+2r-1, lanes c+2r..c+2r+c-1
-    ins = []
-    for j in range(r):
-        for a in range(c):
-            ins.append((a, c + j, c + r + j, f"%{c + 2 * r + a}"))
-    tl = ", ".join(f"int L{a}" for a in range(c))
-    args = ", ".join(f"T& a{a}" for a in range(c))
-    outs = ", ".join(f'"+v"(a{a})' for a in range(c))
-    ins_ops = ", ".join([f'"v"(s[{j}])' for j in range(r)] + [f'"v"(m[{j}])' for j in range(r)] +
-                        [f'"n"(L{a})' for a in range(c)])
-    out = [f"template <{tl}, class T>",
-           f"__device__ __forceinline__ void dpp_sa{r}x{c}({args}, const T* s, const T* m) {{"]
-    for t, mn in (("double", "v_fmac_f64_dpp"), ("float", "v_fmac_f32_dpp")):
-        kw = "if constexpr" if t == "double" else "else"
-        cond = f" (sizeof(T) == 8)" if t == "double" else ""
-        out.append(f"  {kw}{cond}")
-        out.append(f'    asm("{body(ins, c, mn)}"')
-        out.append(f"        : {outs}")
-        out.append(f"        : {ins_ops});")
-    out.append("}")
-    return "\n".join(out)
+def col_block(name, nq, cols, r, arrays, src_of, m_of, doc):
+    """acc c += sum_r bcast(src_of(c, r), lam(c)) * m_of(c, r): broadcast lane per column."""
+    terms = [[(src_of(c, j), m_of(c, j), lam(nq, c)) for c in cols] for j in range(r)]
+    return Block(name, len(cols), arrays, terms, doc)
 
 
-def gen_sb(name, c):
-    lanes = LISTS[name]
-    r = len(lanes)
-    # operands: acc 0..c-1, s c..2c-1, m 2c..2c+r-1
-    ins = []
-    for j in range(r):
-        for a in range(c):
-            ins.append((a, c + a, 2 * c + j, str(lanes[j])))
-    args = ", ".join(f"T& a{a}" for a in range(c)) + ", " + ", ".join(f"T s{a}" for a in range(c))
-    outs = ", ".join(f'"+v"(a{a})' for a in range(c))
-    ins_ops = ", ".join([f'"v"(s{a})' for a in range(c)] + [f'"v"(m[{j}])' for j in range(r)])
-    out = ["template <class T>",
-           f"__device__ __forceinline__ void dpp_sb_{name}_{c}({args}, const T* m) {{"]
-    for t, mn in (("double", "v_fmac_f64_dpp"), ("float", "v_fmac_f32_dpp")):
-        kw = "if constexpr" if t == "double" else "else"
-        cond = f" (sizeof(T) == 8)" if t == "double" else ""
-        out.append(f"  {kw}{cond}")
-        out.append(f'    asm("{body(ins, c, mn)}"')
-        out.append(f"        : {outs}")
-        out.append(f"        : {ins_ops});")
-    out.append("}")
-    return "\n".join(out)
+def lane_block(name, lanes, c, arrays, doc):
+    """acc a += sum_r bcast(s_a, lanes[r]) * m[r]: one broadcast source per accumulator."""
+    terms = [[(f"s[{a}]", f"m[{j}]", lanes[j]) for a in range(c)] for j in range(len(lanes))]
+    return Block(name, c, arrays, terms, doc)
+
+
+def blocks():
+    B = []
+    # ---- whole body (NQ = 7) ----
+    # S = H [A B]: S[c] += sum_r bcast(W[r], lam(c)) * H[7 + r]; columns 16, 17 from W2
+    for nm, cols in (("a", range(0, 6)), ("b", range(6, 12)), ("c", range(12, 18))):
+        B.append(col_block(
+            f"wb_s_{nm}", 7, list(cols), 7, ["w1", "w2", "h"],
+            lambda c, j: f"w1[{j}]" if c < 16 else f"w2[{j}]", lambda c, j: f"h[{j}]",
+            f"whole body S = H [A B], columns {cols.start}..{cols.stop - 1}"))
+    # stance rank-2 terms: Q[.][d] += sum_z bcast(G2[z], lam(d)) * cc[z]
+    for nm, cols in (("a", range(0, 6)), ("b", range(6, 12))):
+        B.append(col_block(f"wb_st_{nm}", 7, list(cols), 2, ["g", "cc"],
+                           lambda c, j: f"g[{j}]", lambda c, j: f"cc[{j}]",
+                           f"whole body C'lyyC / D'lyyC terms, columns {cols.start}..{cols.stop - 1}"))
+    # columns 12..17 and the second control set (rows 16, 17: only columns 16, 17)
+    terms = []
+    for j in range(2):
+        rnd = [(f"g[{j}]", f"cc[{j}]", lam(7, c)) for c in range(12, 16)]
+        rnd += [(f"g2[{j}]", f"cc[{j}]", lam(7, c)) for c in (16, 17)]
+        rnd += [(f"g2[{j}]", f"cc2[{j}]", lam(7, c)) for c in (16, 17)]
+        terms.append(rnd)
+    B.append(Block("wb_st_c", 8, ["g", "g2", "cc", "cc2"], terms,
+                   "whole body stance terms, columns 12..17 (6 accumulators) and the control rows 2, 3"
+                   " (2 accumulators)"))
+    # H update: H[rho][j] += sum_a bcast(Qxu[a], lam(j)) * K[a]
+    for nm, cols in (("a", range(0, 7)), ("b", range(7, 14))):
+        B.append(col_block(f"wb_h_{nm}", 7, list(cols), 4, ["qxu", "k"],
+                           lambda c, j: f"qxu[{j}]", lambda c, j: f"k[{j}]",
+                           f"whole body H update, columns {cols.start}..{cols.stop - 1}"))
+    # impact step H = T Px: H[i][j] += sum_m bcast(Pc[m], lam(j)) * T[m] (m in one half)
+    for nm, cols in (("a", range(0, 7)), ("b", range(7, 14))):
+        B.append(col_block(f"wb_p_{nm}", 7, list(cols), 7, ["pc", "t"],
+                           lambda c, j: f"pc[{j}]", lambda c, j: f"t[{j}]",
+                           f"impact step H = T Px, columns {cols.start}..{cols.stop - 1}, seven m"))
+    # Q = [A B]' S, G column, Px' H2: one broadcast source per accumulator, lanes 2r+1 / 2r
+    odd7, even7 = [1, 3, 5, 7, 9, 11, 13], [0, 2, 4, 6, 8, 10, 12]
+    for c in (3, 6, 7, 8):
+        B.append(lane_block(f"sb_odd7_{c}", odd7, c, ["s", "m"],
+                            f"acc a += sum_r bcast(s[a], 2r + 1) * m[r], r < 7, {c} accumulators"))
+    for c in (7, 8):
+        B.append(lane_block(f"sb_even7_{c}", even7, c, ["s", "m"],
+                            f"acc a += sum_r bcast(s[a], 2r) * m[r], r < 7, {c} accumulators"))
+    # ---- SRB (NQ = 3) ----
+    for nm, cols in (("a", range(0, 5)), ("b", range(5, 10))):
+        B.append(col_block(f"srb_s_{nm}", 3, list(cols), 3, ["w", "h"],
+                           lambda c, j: f"w[{j}]", lambda c, j: f"h[{j}]",
+                           f"SRB S = H [A B], columns {cols.start}..{cols.stop - 1}"))
+    B.append(col_block("srb_h", 3, list(range(6)), 4, ["qxu", "k"],
+                       lambda c, j: f"qxu[{j}]", lambda c, j: f"k[{j}]", "SRB H update"))
+    for c in (5, 6):
+        B.append(lane_block(f"sb_odd3_{c}", [1, 3, 5], c, ["s", "m"],
+                            f"acc a += sum_r bcast(s[a], 2r + 1) * m[r], r < 3, {c} accumulators"))
+    return B
 
 
 def main():
@@ -102,11 +156,8 @@ def main():
     print()
     print("namespace MHPC_NS {")
     print()
-    for r, c in SA:
-        print(gen_sa(r, c))
-        print()
-    for name, c in SB:
-        print(gen_sb(name, c))
+    for b in blocks():
+        print(b.emit())
         print()
     print("}  // namespace MHPC_NS")
 
