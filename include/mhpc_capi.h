@@ -190,7 +190,11 @@ int mhpc_default_cost_weights(mhpc_cost_weights* w);
 int mhpc_default_constraint_params(mhpc_constraint_params* c);
 /* Replace / read the handle's parameters; take effect from the next mhpc_initialize /
  * mhpc_update_problem (AL / ReB initial values) and mhpc_solve (weights, limits).  Every
- * entry must be finite, weights >= 0, torque_limit > 0, delta and delta_min > 0. */
+ * entry must be finite, weights >= 0, torque_limit > 0, friction_coeff >= 0,
+ * 0 < delta_min <= delta.  Constraint parameters set on an initialized handle make
+ * mhpc_solve return MHPC_ERR_STATE until mhpc_initialize or mhpc_update_problem has applied
+ * their initial values (a solve would otherwise run the new limits with the old AL / ReB
+ * state). */
 int mhpc_set_cost_weights(mhpc_handle* h, const mhpc_cost_weights* w);
 int mhpc_get_cost_weights(mhpc_handle* h, mhpc_cost_weights* w);
 int mhpc_set_constraint_params(mhpc_handle* h, const mhpc_constraint_params* c);

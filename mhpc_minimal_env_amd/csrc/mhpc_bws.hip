@@ -204,6 +204,13 @@ struct RowCtx {
 };
 
 __device__ __forceinline__ bool go(const RowCtx& r) { return r.live && !r.failed; }
+
+// Outputs of a knot awaiting their store.
+struct PendingKnot {
+  bool ok;
+  int k;
+  real K[4], du[4], G;
+};
 __device__ __forceinline__ bool any_go(const RowCtx& r) {
   return __builtin_amdgcn_ballot_w64(go(r)) != 0;
 }
@@ -247,16 +254,18 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
   const int c1 = rho;            // record column of W1 (0..15)
   const int c2 = 16 + (t & 1);   // second set: control columns 2, 3 (lanes 14, 15)
   const int cq = t < NCS ? t : 0;
+  // (the nominal state first: the wait for the last load of a knot then never covers the
+  // stores of the previous knot, which share gfx950's in-order VM counter)
   auto load = [&](int k) {
+    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    pxn = tk[xi];
+    ppos = pos[k];
     const real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+    pcv = rec[PS_JAC + cq];
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr1[r] = rec[c1 * 9 + r];
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr2[r] = rec[c2 * 9 + r];
-    pcv = rec[PS_JAC + cq];
-    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
-    pxn = tk[xi];
-    ppos = pos[k];
   };
   real H[14], Gv;
   {
@@ -266,6 +275,26 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     Gv = rl.Gs[hr];
   }
   const int cr = rho;  // column of M read in the transpose (Qxu columns for lanes 14, 15)
+  // The outputs (K, du, G) of a knot are stored one knot later, right before the next
+  // prefetch: every global operation of a knot is then issued together after the wait for the
+  // previous prefetch, and the next such wait (a knot later) finds the stores retired --
+  // gfx950 counts loads and stores on one in-order VM counter.
+  PendingKnot pend;
+  pend.ok = false;
+  auto store_pending = [&]() {
+    if (pend.ok) {
+      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
+      if (xl) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = pend.K[a];
+        d.G[rec * 14 + rho] = pend.G;
+      } else if (t == 14) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+      }
+    }
+    pend.ok = false;
+  };
   if (N >= 2) load(N - 2);
   for (int k = N - 2; k >= 0; --k) {
     // ---- the knot's derivatives (prefetched) ----
@@ -274,10 +303,16 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     for (int r = 0; r < 7; ++r) W1[r] = __builtin_fma(pr1[r], dt, base[r]);
 #pragma unroll
     for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(pr2[r], dt, real(0.0));
-    G2o[0] = STANCE ? pr1[NR - 2] : real(0.0);
-    G2o[1] = STANCE ? pr1[NR - 1] : real(0.0);
-    G22[0] = STANCE ? pr2[NR - 2] : real(0.0);
-    G22[1] = STANCE ? pr2[NR - 1] : real(0.0);
+    // C, D rows: copied out of the prefetch registers (a fresh value each, so the prefetch
+    // buffer is dead before it is reloaded; a buffer live across its own reload costs a copy
+    // at the back edge that waits for every outstanding memory operation, stores included)
+    G2o[0] = G2o[1] = G22[0] = G22[1] = real(0.0);
+    if (STANCE) {
+      asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
+      asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
+      asm volatile("" : "=v"(G22[0]) : "0"(pr2[NR - 2]));
+      asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
+    }
     // cost derivatives: lane q of the row holds entry q of (lu, luu, ly, lyy)
     real luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
     const real lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
@@ -288,7 +323,8 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     }
     const real rxi = rho == 0 ? ppos : rxc;
     const real lx = w2 * (pxn - rxi);
-    const real l1 = xl ? lx : ((t & 1) ? lu1 : lu0);
+    const real lu01 = (t & 1) ? lu1 : lu0;
+    const real l1 = xl ? lx : lu01;
     const real l2 = (t & 1) ? lu3 : lu2;
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
@@ -302,6 +338,7 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     asm volatile("" ::"v"(G2o[0]), "v"(G2o[1]), "v"(G22[0]), "v"(G22[1]), "v"(luu[0]),
                  "v"(luu[1]), "v"(luu[2]), "v"(luu[3]), "v"(ly[0]), "v"(ly[1]), "v"(lyy[0]),
                  "v"(lyy[1]), "v"(lyy[2]), "v"(lyy[3]));
+    store_pending();
     if (k > 0) load(k - 1);
 
     // ---- S = H [A B] (lane: row rho of S) and Q = [A B]' S + ... (lane: row rho of Q),
@@ -356,10 +393,12 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     // ---- Qxx transpose through LDS (symmetrisation, MHPC_CompoundTypes.h:134) ----
 #pragma unroll
     for (int j = 0; j < 16; ++j) rl.M[rho * MP + j] = Q[j];
-    {
-      real* dq = &rl.M[rho * MP + rho];
-      *dq = *dq + dg2;
-    }
+    // + 2 (lxx + reg) on the diagonal of the transposed copy: an LDS atomic add, in order with
+    // this wave's other LDS operations, no round trip
+    atomicAdd(&rl.M[rho * MP + rho], dg2);
+    real T[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[j] = rl.M[j * MP + cr];
 
     // ---- the control block on every lane ----
     wk q[4][4], Qu[4];
@@ -414,10 +453,7 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     // H = sym(Qxx) - Qux' Quu^-1 Qux: H[rho][j] = Qs[j] + sum_a K[a] Qux[a][j]
     wk Hn[14];
 #pragma unroll
-    for (int j = 0; j < 14; ++j) {
-      const real tj = rl.M[j * MP + cr];
-      Hn[j] = wk((Q[j] + tj) / 2);
-    }
+    for (int j = 0; j < 14; ++j) Hn[j] = wk((Q[j] + T[j]) / 2);
     wb_h_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Qxu, K);
     wb_h_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Qxu, K);
 #pragma unroll
@@ -425,21 +461,20 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
     Gv = real(Gn);
     // ---- outputs of knot k (only while the row's attempt is alive) ----
     const bool ok = gate && psd;
-    if (ok) {
-      const size_t rec = (size_t)b * sp.NK + ko + k;
-      if (xl) {
+    // outputs of knot k, stored at the top of the next knot (see store_pending)
+    pend.ok = ok;
+    pend.k = k;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = real(K[a]);
-        d.G[rec * 14 + rho] = real(Gn);
-      } else if (t == 14) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = real(du[a]);
-      }
-      rc.dV += acc(dv);
+    for (int a = 0; a < 4; ++a) {
+      pend.K[a] = real(K[a]);
+      pend.du[a] = real(du[a]);
     }
+    pend.G = real(Gn);
+    if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
     if (!any_go(rc)) break;
   }
+  store_pending();
   // value function of knot 0 back to LDS
   __syncthreads();
   if (xl) {
@@ -513,11 +548,11 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
   real pxs[2], pus[4], pv, ppos;
   auto load = [&](int k) {
     const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    ppos = pos[k];
+    pv = tk[cj];
     pxs[0] = tk[0]; pxs[1] = tk[1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) pus[c] = tk[6 + c];
-    pv = tk[cj];
-    ppos = pos[k];
   };
   real H[6], Gv;
   {
@@ -527,6 +562,22 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     Gv = rl.Gs[hr];
   }
   const int cr = rho < 10 ? rho : 0;
+  PendingKnot pend;  // outputs stored one knot later (see sweep_wb)
+  pend.ok = false;
+  auto store_pending = [&]() {
+    if (pend.ok) {
+      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
+      if (xl) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 6 + rho] = pend.K[a];
+        d.G[rec * 14 + rho] = pend.G;
+      } else if (t == 6) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+      }
+    }
+    pend.ok = false;
+  };
   if (N >= 2) load(N - 2);
   for (int k = N - 2; k >= 0; --k) {
     real W[3];
@@ -538,6 +589,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     asm volatile("" ::"v"(W[2]), "v"(l1));  // see sweep_wb
+    store_pending();
     if (k > 0) load(k - 1);
     real S[10];
 #pragma unroll
@@ -561,10 +613,10 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     }
 #pragma unroll
     for (int j = 0; j < 10; ++j) rl.M[(rho & 15) * MP + j] = Q[j];
-    {
-      real* dq = &rl.M[(rho & 15) * MP + (rho & 15)];
-      *dq = *dq + dg2;
-    }
+    atomicAdd(&rl.M[(rho & 15) * MP + (rho & 15)], dg2);  // see sweep_wb
+    real T[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) T[j] = rl.M[j * MP + cr];
     real q[4][4], Qu[4];
     q[0][0] = rbc<6>(Q[6]); q[0][1] = rbc<6>(Q[7]); q[0][2] = rbc<6>(Q[8]); q[0][3] = rbc<6>(Q[9]);
     q[1][1] = rbc<7>(Q[7]); q[1][2] = rbc<7>(Q[8]); q[1][3] = rbc<7>(Q[9]);
@@ -612,27 +664,25 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
     real Hn[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) Hn[j] = (Q[j] + rl.M[j * MP + cr]) / 2;
+    for (int j = 0; j < 6; ++j) Hn[j] = (Q[j] + T[j]) / 2;
     srb_h(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Qxu, K);
 #pragma unroll
     for (int j = 0; j < 6; ++j) H[j] = Hn[j];
     Gv = Gn;
     const bool ok = gate && psd;
-    if (ok) {
-      const size_t rec = (size_t)b * sp.NK + ko + k;
-      if (xl) {
+    pend.ok = ok;
+    pend.k = k;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 6 + rho] = K[a];
-        d.G[rec * 14 + rho] = Gn;
-      } else if (t == 6) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = du[a];
-      }
-      rc.dV += acc(dv);
+    for (int a = 0; a < 4; ++a) {
+      pend.K[a] = K[a];
+      pend.du[a] = du[a];
     }
+    pend.G = Gn;
+    if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
     if (!any_go(rc)) break;
   }
+  store_pending();
   __syncthreads();
   if (xl) {
 #pragma unroll
@@ -804,6 +854,13 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
   __syncthreads();
 }
 
+// Waves per SIMD the register allocator leaves room for in the SRB half: it runs beside the
+// partials; capped at 256 VGPRs (A/B round 4: a 168-VGPR cap that lets a 340-VGPR partials
+// wave share the SIMD spills the SRB knot to scratch and loses 2 % of a batch-1024 step).
+#ifndef MHPC_BWS_SRB_WAVES
+#define MHPC_BWS_SRB_WAVES 2
+#endif
+
 // RPW problems per wave (rows 0..RPW-1 of the wave; the others idle).
 //
 // PART 0: the whole sweep with its regularisation retries (MultiPhaseDDP.cpp:196-241).
@@ -812,7 +869,8 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
 // PART 2: the WB phases of the first attempt (rows whose SRB part passed), then the same
 // retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
 template <int RPW, int PART>
-__global__ __launch_bounds__(64, 1) void k_bws(SolveParams sp, DevBufs d, real update_reg) {
+__global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(SolveParams sp, DevBufs d,
+                                                                    real update_reg) {
   __shared__ BwsLds sh;
   const int row = threadIdx.x >> 4;
   RowCtx rc;

@@ -84,6 +84,10 @@ struct Handle {
   hipEvent_t evfork = nullptr, evjoin = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool x0_set = false, initialized = false, solved = false, x0_changed = false;
+  // constraint parameters replaced after the last initialize / update_problem: their AL / ReB
+  // initial values reach the problems' state only there, so a solve in between
+  // would mix new limits with old initial values -- refused until then
+  bool params_changed = false;
   float solve_ms = 0;
   unsigned long long* dcnt = nullptr;  // reduced counters of the batch [NCNT]
   unsigned long long cnt[NCNT] = {};
@@ -296,13 +300,18 @@ int api_set_constraint_params(Handle* h, const mhpc_constraint_params* c) {
   for (size_t i = 0; i < sizeof(mhpc_constraint_params) / sizeof(double); ++i)
     if (!std::isfinite(v[i])) return fail(MHPC_ERR_INVALID, "constraint parameters must be finite");
   if (!(c->torque_limit > 0)) return fail(MHPC_ERR_INVALID, "torque_limit must be > 0");
+  if (!(c->friction_coeff >= 0))
+    return fail(MHPC_ERR_INVALID, "friction_coeff must be >= 0 (a negative one inverts the GRF cone)");
   for (int m = 0; m < 4; ++m) {
     if (!(c->delta[m] > 0) || !(c->delta_min[m] > 0))
       return fail(MHPC_ERR_INVALID, "delta and delta_min must be > 0");
+    if (c->delta_min[m] > c->delta[m])
+      return fail(MHPC_ERR_INVALID, "delta_min must not exceed delta (the AL update only shrinks delta)");
     if (c->sigma[m] < 0 || c->eps_torque[m] < 0 || c->eps_grf[m] < 0)
       return fail(MHPC_ERR_INVALID, "sigma and the ReB weights must be >= 0");
   }
   put_constraints(h->sp.cw, *c);
+  if (h->initialized) h->params_changed = true;
   return MHPC_OK;
 }
 int api_get_constraint_params(Handle* h, mhpc_constraint_params* c) {
@@ -513,6 +522,7 @@ int api_initialize(Handle* h) {
   if (rc) return rc;
   h->initialized = true;
   h->x0_changed = false;
+  h->params_changed = false;
   h->solved = false;
   return MHPC_OK;
 }
@@ -724,6 +734,9 @@ int api_solve(Handle* h, int32_t* status) {
   if (h->solved) return fail(MHPC_ERR_STATE, "solve already ran: call mhpc_initialize or mhpc_update_problem");
   if (h->x0_changed)
     return fail(MHPC_ERR_STATE, "x0 changed: call mhpc_initialize or mhpc_update_problem first");
+  if (h->params_changed)
+    return fail(MHPC_ERR_STATE,
+                "constraint parameters changed: call mhpc_initialize or mhpc_update_problem first");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   int rc = solve_async(h);
@@ -783,7 +796,11 @@ int api_get_phase(Handle* h, int phase, int first, int count, double* x, double*
   std::vector<real> buf;
   int rc;
   if (x || u || y) {
-    HIPCHK(launch_export(sp, h->d, h->stream));
+    // export only the requested problems (a caller looping over problems would otherwise
+    // export the whole batch per call): the block's arrays as the solve's sub-batches see them
+    SolveParams sub = sp;
+    sub.B = count;
+    HIPCHK(launch_export(sub, block_bufs(h->d, sp, b0), h->stream));
     if ((rc = copy_rows(h, h->d.out, KS, ko, N, b0, B, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k) {
@@ -970,6 +987,7 @@ int api_update_problem(Handle* h, const mhpc_gait* gait) {
   h->need_full = true;
   h->solved = false;
   h->x0_changed = false;
+  h->params_changed = false;
   return MHPC_OK;
 }
 
