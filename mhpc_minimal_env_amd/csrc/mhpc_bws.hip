@@ -32,9 +32,10 @@
 // finite filler that no real row reads.
 //
 // The 4x4 control block is assembled on every lane (row broadcasts), tested for
-// positive-definiteness (unpivoted LDL^T, tests/test_psd_verdict.py) and inverted by 2x2
-// cofactors; Q is symmetric by construction in its control block and Qxx is symmetrised
-// through one LDS transpose per knot, as the reference does (MHPC_CompoundTypes.h:133-134).
+// positive-definiteness (unpivoted LDL^T of Quu - 1e-9 I, tests/test_psd_verdict.py) and
+// applied through its own LDL^T factor; Q is symmetric by construction in its control block
+// and Qxx is symmetrised through one LDS transpose per knot, as the reference does
+// (MHPC_CompoundTypes.h:133-134).
 // The arithmetic is the reference's up to summation order (parity: tests/test_gpu_solve.py);
 // every launch shape (problems per wave) runs the same per-row code, so all of them agree bit
 // for bit (tests/test_gpu_variants.py).
@@ -141,42 +142,40 @@ __device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
   return !neg;
 }
 
-// Inverse of a symmetric 4x4 matrix by 2x2 cofactors (Laplace expansion along the first two
-// rows); the upper triangle is computed and mirrored, so the result is exactly symmetric --
-// the reference symmetrises Quu^-1 explicitly (MHPC_CompoundTypes.h:133).
+// Quu^-1 applied by an LDL^T factorisation of the symmetric 4x4 control block (no explicit
+// inverse: the reference forms (Quu^-1 + Quu^-T) / 2 and multiplies, MHPC_CompoundTypes.h
+// :133-139; the factor solves the same systems -- up to rounding -- in about half the
+// instructions).  Only used when Quu - 1e-9 I passed the PSD test, so the pivots are > 0.
 template <class T>
-__device__ __forceinline__ void inverse4_sym(const T (&m)[4][4], T (&v)[4][4]) {
-  const T s0 = m[0][0] * m[1][1] - m[1][0] * m[0][1];
-  const T s1 = m[0][0] * m[1][2] - m[1][0] * m[0][2];
-  const T s2 = m[0][0] * m[1][3] - m[1][0] * m[0][3];
-  const T s3 = m[0][1] * m[1][2] - m[1][1] * m[0][2];
-  const T s4 = m[0][1] * m[1][3] - m[1][1] * m[0][3];
-  const T s5 = m[0][2] * m[1][3] - m[1][2] * m[0][3];
-  const T c5 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
-  const T c4 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
-  const T c3 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
-  const T c2 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
-  const T c1 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
-  const T c0 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
-  const T det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
-  const T r = recip(det);
-  v[0][0] = (m[1][1] * c5 - m[1][2] * c4 + m[1][3] * c3) * r;
-  v[0][1] = (-m[0][1] * c5 + m[0][2] * c4 - m[0][3] * c3) * r;
-  v[0][2] = (m[3][1] * s5 - m[3][2] * s4 + m[3][3] * s3) * r;
-  v[0][3] = (-m[2][1] * s5 + m[2][2] * s4 - m[2][3] * s3) * r;
-  v[1][1] = (m[0][0] * c5 - m[0][2] * c2 + m[0][3] * c1) * r;
-  v[1][2] = (-m[3][0] * s5 + m[3][2] * s2 - m[3][3] * s1) * r;
-  v[1][3] = (m[2][0] * s5 - m[2][2] * s2 + m[2][3] * s1) * r;
-  v[2][2] = (m[3][0] * s4 - m[3][1] * s2 + m[3][3] * s0) * r;
-  v[2][3] = (-m[2][0] * s4 + m[2][1] * s2 - m[2][3] * s0) * r;
-  v[3][3] = (m[2][0] * s3 - m[2][1] * s1 + m[2][2] * s0) * r;
-  v[1][0] = v[0][1];
-  v[2][0] = v[0][2];
-  v[3][0] = v[0][3];
-  v[2][1] = v[1][2];
-  v[3][1] = v[1][3];
-  v[3][2] = v[2][3];
-}
+struct Ldl4 {
+  T l10, l20, l30, l21, l31, l32, r0, r1, r2, r3;  // unit lower factor, 1 / pivots
+  __device__ __forceinline__ explicit Ldl4(const T (&q)[4][4]) {
+    r0 = recip(q[0][0]);
+    l10 = q[1][0] * r0;
+    l20 = q[2][0] * r0;
+    l30 = q[3][0] * r0;
+    r1 = recip(q[1][1] - l10 * q[1][0]);
+    const T u21 = q[2][1] - l20 * q[1][0], u31 = q[3][1] - l30 * q[1][0];
+    l21 = u21 * r1;
+    l31 = u31 * r1;
+    r2 = recip((q[2][2] - l20 * q[2][0]) - l21 * u21);
+    const T u32 = (q[3][2] - l30 * q[2][0]) - l31 * u21;
+    l32 = u32 * r2;
+    r3 = recip(((q[3][3] - l30 * q[3][0]) - l31 * u31) - l32 * u32);
+  }
+  // x = -Quu^-1 b
+  __device__ __forceinline__ void neg_solve(const T (&b)[4], T (&x)[4]) const {
+    const T z0 = b[0];
+    const T z1 = b[1] - l10 * z0;
+    const T z2 = (b[2] - l20 * z0) - l21 * z1;
+    const T z3 = ((b[3] - l30 * z0) - l31 * z1) - l32 * z2;
+    const T w0 = -(z0 * r0), w1 = -(z1 * r1), w2 = -(z2 * r2), w3 = -(z3 * r3);
+    x[3] = w3;
+    x[2] = w2 - l32 * x[3];
+    x[1] = (w1 - l21 * x[2]) - l31 * x[3];
+    x[0] = ((w0 - l10 * x[1]) - l20 * x[2]) - l30 * x[3];
+  }
+};
 
 // Per-row LDS: the knot's Q rows for the Qxx transpose, and the value function at phase
 // boundaries (row-major by state index, pitch MP reals: 16-byte aligned rows).
@@ -422,30 +421,17 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
         for (int c = 0; c < 4; ++c) A[a * 4 + c] = real(q[a][c]) - (a == c ? sp.eps9 : real(0.0));
       psd = ldlt_nopiv_is_positive4(A);
     }
-    wk Qi[4][4];
-    inverse4_sym(q, Qi);
+    const Ldl4<wk> F(q);
     // du = -Quu^-1 Qu, dV += -Qu' Quu^-1 Qu (no 1/2, MHPC_CompoundTypes.h:137-142)
     wk du[4], dv = wk(0.0);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      wk s = wk(0.0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qu[c];
-      du[a] = -s;
-    }
+    F.neg_solve(Qu, du);
 #pragma unroll
     for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
     // K = -Quu^-1 Qux: column rho on lane rho (Qux[m][rho] = Q[rho][14 + m], own)
     wk Qxu[4], K[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) Qxu[m] = wk(Q[14 + m]);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      wk s = wk(0.0);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) s += Qi[a][m] * Qxu[m];
-      K[a] = -s;
-    }
+    F.neg_solve(Qxu, K);
     // G = Qx - Qux' Quu^-1 Qu
     wk Gn = wk(Qv1);
 #pragma unroll
@@ -637,28 +623,15 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
         for (int c = 0; c < 4; ++c) A[a * 4 + c] = q[a][c] - (a == c ? sp.eps9 : real(0.0));
       psd = ldlt_nopiv_is_positive4(A);
     }
-    real Qi[4][4];
-    inverse4_sym(q, Qi);
+    const Ldl4<real> F(q);
     real du[4], dv = real(0.0);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      real s = real(0.0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qu[c];
-      du[a] = -s;
-    }
+    F.neg_solve(Qu, du);
 #pragma unroll
     for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
     real Qxu[4], K[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) Qxu[c] = Q[6 + c];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      real s = real(0.0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += Qi[a][c] * Qxu[c];
-      K[a] = -s;
-    }
+    F.neg_solve(Qxu, K);
     real Gn = Qv1;
 #pragma unroll
     for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
