@@ -244,6 +244,8 @@ void mhpc_destroy(mhpc_handle* h);
 #define MHPC_VARIANT_BWS_ROWS4 1      /*   four problems per wave (one per 16-lane row) */
 #define MHPC_VARIANT_BWS_ROWS2 2      /*   two problems per wave (rows 0, 1) */
 #define MHPC_VARIANT_BWS_ROWS1 3      /*   one problem per wave (row 0) */
+#define MHPC_VARIANT_BWS_PAIRS2 4     /*   two problems per wave, two rows each in the
+                                         whole-body phases (default up to 2048 problems) */
 #define MHPC_VARIANT_RO 1             /* which: line-search rollouts */
 #define MHPC_VARIANT_RO_PAIR 1        /*   two-wave pipeline, a lane pair per candidate */
 #define MHPC_VARIANT_RO_PIPE_STAGED 2 /*   two-wave pipeline, LDS-staged operands */

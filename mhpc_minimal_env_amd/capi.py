@@ -25,7 +25,7 @@ MHPC_ERR_INVALID = 1
 # mhpc_set_kernel_variant (include/mhpc_capi.h)
 MHPC_VARIANT_BWS = 0
 MHPC_VARIANT_RO = 1
-BWS_VARIANTS = {"auto": 0, "rows4": 1, "rows2": 2, "rows1": 3}
+BWS_VARIANTS = {"auto": 0, "rows4": 1, "rows2": 2, "rows1": 3, "pairs2": 4}
 RO_VARIANTS = {"auto": 0, "pair": 1, "pipe_staged": 2, "pipe": 3, "fused_staged": 4, "fused": 5}
 MHPC_VARIANT_OVERLAP = 2
 OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}

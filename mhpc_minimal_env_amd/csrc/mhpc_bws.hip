@@ -104,6 +104,36 @@ __device__ __forceinline__ double qperm(double v) {
   return __hiloint2double(qperm_i(__double2hiint(v)), qperm_i(__double2loint(v)));
 }
 __device__ __forceinline__ float qperm(float v) { return __int_as_float(qperm_i(__float_as_int(v))); }
+// Two-row layout: on rows 1 and 3 (row B of a problem) an even lane takes the odd lane above
+// it (quad_perm [1,1,3,3], row_mask 0b1010); rows 0 and 2 keep their own value.
+__device__ __forceinline__ int qshift_rowB_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0xF5, 0xA, 0xF, false);
+}
+__device__ __forceinline__ double qshift_rowB(double v) {
+  return __hiloint2double(qshift_rowB_i(__double2hiint(v)), qshift_rowB_i(__double2loint(v)));
+}
+__device__ __forceinline__ float qshift_rowB(float v) {
+  return __int_as_float(qshift_rowB_i(__float_as_int(v)));
+}
+// Row pair exchange (v_permlane16_swap): a = row A's value, b = row B's value, on both rows.
+__device__ __forceinline__ void row_pair_swap_i(unsigned v, unsigned& a, unsigned& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void row_pair_swap(double v, double& a, double& b) {
+  unsigned ahi, bhi, alo, blo;
+  row_pair_swap_i((unsigned)__double2hiint(v), ahi, bhi);
+  row_pair_swap_i((unsigned)__double2loint(v), alo, blo);
+  a = __hiloint2double((int)ahi, (int)alo);
+  b = __hiloint2double((int)bhi, (int)blo);
+}
+__device__ __forceinline__ void row_pair_swap(float v, float& a, float& b) {
+  unsigned ua, ub;
+  row_pair_swap_i((unsigned)__float_as_int(v), ua, ub);
+  a = __int_as_float((int)ua);
+  b = __int_as_float((int)ub);
+}
 
 // 1 / a by the hardware estimate and two Newton steps (within an ulp of the division; the
 // IEEE division sequence is twice the instructions and latency)
@@ -193,6 +223,8 @@ struct BwsLds {
 struct RowCtx {
   int b;       // problem (clamped into the batch for a spare row)
   int t;       // lane within the row
+  int rp;      // row of the problem this lane's row is (0, or 1 in the two-row layout)
+  int lt, nl;  // lane within the problem's rows, lanes per problem (16 or 32)
   bool act;    // the row holds an active problem in this launch
   bool live;   // the row takes part in the current sweep attempt
   bool failed; // ... and its attempt has failed (PSD test) -- sticky for the attempt
@@ -471,6 +503,250 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------------------
+// Whole-body phase, two rows per problem (sweep_wb2, the launch shape for batches that leave
+// SIMDs idle).  Both rows hold the value function (row rho(t) on lane t) and the control
+// columns 14..17; row A computes the configuration columns 0..6 of S and Q, row B the
+// velocity columns 7..13 in the same register slots.  Row B's broadcast copy of [A B] puts
+// column 7 + s on lane 2 s, so both rows run the same instruction stream with the same DPP
+// lane immediates (the S/Q blocks shrink from 18 + 1 to 11 + 1 columns per row).  The
+// transpose writes each row's half of Qxx to the shared LDS block; each row updates its seven
+// columns of H, and one v_permlane16_swap per word gives both rows the full rows of H.  Every
+// entry is computed with the one-row sweep's operations in the same order, so the two
+// layouts agree bit for bit (tests/test_gpu_variants.py).
+template <bool STANCE>
+__device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+                          RowCtx& rc, int p) {
+  using R = Rows<7>;
+  using wk = wreal;
+  const int t = rc.t, b = rc.b, rp = rc.rp;
+  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+  const real dt = sp.dt[p];
+  const int rho = R::rho(t);
+  const bool xl = t < 14;
+  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
+  const real coefS = rp ? dt : real(1.0);  // S init: column s (row A) / 7 + s (row B)
+  // broadcast column of the lane: its own (row A, odd lanes, lanes 14 / 15) or, on row B's
+  // even lanes 2 s, the velocity column 7 + s
+  const int cb = (rp && xl && !(t & 1)) ? 7 + (t >> 1) : rho;
+  real base[7], baseb[7];
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    base[r] = rho == 7 + r ? real(1.0) : real(0.0);
+    baseb[r] = cb == 7 + r ? real(1.0) : real(0.0);
+  }
+  const int xi = xl ? rho : 0;
+  const real w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
+  const real rxc = xi == 1 ? sp.height : xi == 2 ? real(0.0)
+                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : real(0.0);
+  // lxx + reg on the diagonal, added by the row that owns the diagonal's column
+  const bool own_diag = xl && ((rho < 7) == (rp == 0));
+  const real dg2 = own_diag ? 2 * (w2 + rc.reg) : real(0.0);
+  // LDS column of matrix column c (row B's half starts 16-byte aligned)
+  auto mcol = [](int c) { return c < 7 ? c : c + 1; };
+  const real* pos = d.refpos + (size_t)b * sp.NK + ko;
+  constexpr int NR = STANCE ? 9 : 7;
+  constexpr int NCS = STANCE ? 14 : 8;
+  real pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;
+  const int c2 = 16 + (t & 1);
+  const int cq = t < NCS ? t : 0;
+  auto load = [&](int k) {
+    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    pxn = tk[xi];
+    ppos = pos[k];
+    const real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
+    pcv = rec[PS_JAC + cq];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pr1[r] = rec[rho * 9 + r];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) prb[r] = rec[cb * 9 + r];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pr2[r] = rec[c2 * 9 + r];
+  };
+  real H[14], Gv;
+  {
+    const int hr = xl ? rho : 0;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) H[j] = rl.M[hr * MP + j];
+    Gv = rl.Gs[hr];
+  }
+  const int cr = xl ? mcol(rho) : 0;   // LDS column read in the transpose
+  const int wo = rp ? 8 : 0;            // LDS column of the row's first Q column
+  const int jr = rp ? 7 : 0;            // first matrix row of the row's H columns
+  PendingKnot pend;
+  pend.ok = false;
+  auto store_pending = [&]() {
+    if (pend.ok) {
+      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
+      if (xl) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = pend.K[a];
+        d.G[rec * 14 + rho] = pend.G;
+      } else if (t == 14) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+      }
+    }
+    pend.ok = false;
+  };
+  if (N >= 2) load(N - 2);
+  for (int k = N - 2; k >= 0; --k) {
+    real Wo[7], Wb[7], W2[7], G2o[2], G2b[2], G22[2];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      Wo[r] = __builtin_fma(pr1[r], dt, base[r]);
+      Wb[r] = __builtin_fma(prb[r], dt, baseb[r]);
+      W2[r] = __builtin_fma(pr2[r], dt, real(0.0));
+    }
+    G2o[0] = G2o[1] = G2b[0] = G2b[1] = G22[0] = G22[1] = real(0.0);
+    if (STANCE) {  // fresh values (see sweep_wb)
+      asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
+      asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
+      asm volatile("" : "=v"(G2b[0]) : "0"(prb[NR - 2]));
+      asm volatile("" : "=v"(G2b[1]) : "0"(prb[NR - 1]));
+      asm volatile("" : "=v"(G22[0]) : "0"(pr2[NR - 2]));
+      asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
+    }
+    real luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
+    const real lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
+    luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
+    if (STANCE) {
+      ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
+      lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
+    }
+    const real rxi = rho == 0 ? ppos : rxc;
+    const real lx = w2 * (pxn - rxi);
+    const real lu01 = (t & 1) ? lu1 : lu0;
+    const real l1 = xl ? lx : lu01;
+    const real l2 = (t & 1) ? lu3 : lu2;
+    const bool gate = go(rc);
+    rc.kn += gate ? 1 : 0;
+    rc.kn_wb += gate ? 1 : 0;
+    asm volatile("" ::"v"(Wo[0]), "v"(Wo[1]), "v"(Wo[2]), "v"(Wo[3]), "v"(Wo[4]), "v"(Wo[5]),
+                 "v"(Wo[6]), "v"(Wb[0]), "v"(Wb[1]), "v"(Wb[2]), "v"(Wb[3]), "v"(Wb[4]),
+                 "v"(Wb[5]), "v"(Wb[6]), "v"(l1), "v"(l2));
+    asm volatile("" ::"v"(W2[0]), "v"(W2[1]), "v"(W2[2]), "v"(W2[3]), "v"(W2[4]), "v"(W2[5]),
+                 "v"(W2[6]), "v"(G2o[0]), "v"(G2o[1]), "v"(G2b[0]), "v"(G2b[1]), "v"(G22[0]),
+                 "v"(G22[1]));
+    asm volatile("" ::"v"(luu[0]), "v"(luu[1]), "v"(luu[2]), "v"(luu[3]), "v"(ly[0]), "v"(ly[1]),
+                 "v"(lyy[0]), "v"(lyy[1]), "v"(lyy[2]), "v"(lyy[3]));
+    store_pending();
+    if (k > 0) load(k - 1);
+
+    // ---- S and Q, slots 0..6 (the row's half of columns 0..13) and 7..10 (columns 14..17)
+    real S[11], Q[11], Q2[2], Qv1, Qv2;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) S[s] = coefS * H[s];
+#pragma unroll
+    for (int s = 7; s < 11; ++s) S[s] = real(0.0);
+    real cc[2] = {0, 0}, cc2[2] = {0, 0};
+    if (STANCE) {
+#pragma unroll
+      for (int z = 0; z < 2; ++z) {
+        cc[z] = G2o[0] * lyy[z] + G2o[1] * lyy[2 + z];
+        cc2[z] = G22[0] * lyy[z] + G22[1] * lyy[2 + z];
+      }
+    }
+    wb_s_a(S[0], S[1], S[2], S[3], S[4], S[5], Wb, W2, H + 7);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) Q[s] = coef * qperm(S[s]);
+    sb_odd7_6(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], S + 0, Wo);
+    if (STANCE) wb_st_a(Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], G2b, cc);
+    wb2_s_b(S[6], S[7], S[8], S[9], S[10], Wb, W2, H + 7);
+#pragma unroll
+    for (int s = 6; s < 11; ++s) Q[s] = coef * qperm(S[s]);
+    Qv1 = __builtin_fma(coef, qperm(Gv), l1);
+    Q2[0] = real(0.0);
+    Q2[1] = real(0.0);
+    Qv2 = l2;
+    {
+      const real sc[6] = {S[6], S[7], S[8], S[9], S[10], Gv};
+      sb_odd7_6(Q[6], Q[7], Q[8], Q[9], Q[10], Qv1, sc, Wo);
+      const real s2[3] = {S[9], S[10], Gv};
+      sb_odd7_3(Q2[0], Q2[1], Qv2, s2, W2);
+    }
+    if (STANCE) {
+      wb2_st_b(Q[6], Q[7], Q[8], Q[9], Q[10], Q2[0], Q2[1], G2b, G22, cc, cc2);
+      Qv1 = (Qv1 + G2o[0] * ly[0]) + G2o[1] * ly[1];
+      Qv2 = (Qv2 + G22[0] * ly[0]) + G22[1] * ly[1];
+    }
+
+    // ---- Qxx transpose: each row writes its half of the row rho ----
+#pragma unroll
+    for (int s = 0; s < 7; ++s) rl.M[rho * MP + wo + s] = Q[s];
+    atomicAdd(&rl.M[rho * MP + (xl ? mcol(rho) : rho)], dg2);
+    real T[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) T[s] = rl.M[(jr + s) * MP + cr];
+
+    // ---- the control block on every lane (both rows alike) ----
+    wk q[4][4], Qu[4];
+    q[0][0] = rbc<14>(Q[7]); q[0][1] = rbc<14>(Q[8]); q[0][2] = rbc<14>(Q[9]); q[0][3] = rbc<14>(Q[10]);
+    q[1][1] = rbc<15>(Q[8]); q[1][2] = rbc<15>(Q[9]); q[1][3] = rbc<15>(Q[10]);
+    q[2][2] = rbc<14>(Q2[0]); q[2][3] = rbc<14>(Q2[1]); q[3][3] = rbc<15>(Q2[1]);
+    Qu[0] = rbc<14>(Qv1); Qu[1] = rbc<15>(Qv1); Qu[2] = rbc<14>(Qv2); Qu[3] = rbc<15>(Qv2);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[a][a] = q[a][a] + wk(luu[a] + rc.reg);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
+    bool psd;
+    {
+      real A[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) A[a * 4 + c] = real(q[a][c]) - (a == c ? sp.eps9 : real(0.0));
+      psd = ldlt_nopiv_is_positive4(A);
+    }
+    const Ldl4<wk> F(q);
+    wk du[4], dv = wk(0.0);
+    F.neg_solve(Qu, du);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
+    wk Qxu[4], K[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) Qxu[m] = wk(Q[7 + m]);
+    F.neg_solve(Qxu, K);
+    wk Gn = wk(Qv1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
+    // H columns of the row: Qux[a][7 + s] lives on lane 2 s + 1; row B moves it to lane 2 s
+    wk QxuS[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) QxuS[m] = qshift_rowB(Qxu[m]);
+    wk Hn[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) Hn[s] = wk((Q[s] + T[s]) / 2);
+    wb_h_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], QxuS, K);
+    // both rows get both halves
+#pragma unroll
+    for (int s = 0; s < 7; ++s) row_pair_swap(real(Hn[s]), H[s], H[7 + s]);
+    Gv = real(Gn);
+    const bool ok = gate && psd;
+    pend.ok = ok && rp == 0;
+    pend.k = k;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      pend.K[a] = real(K[a]);
+      pend.du[a] = real(du[a]);
+    }
+    pend.G = real(Gn);
+    if (ok) rc.dV += acc(dv);
+    rc.failed = rc.failed || (gate && !psd);
+    if (!any_go(rc)) break;
+  }
+  store_pending();
+  __syncthreads();
+  if (xl && rp == 0) {
+#pragma unroll
+    for (int j = 0; j < 14; ++j) rl.M[rho * MP + j] = H[j];
+    rl.Gs[rho] = Gv;
+  }
+  __syncthreads();
+}
+
 // SRB Jacobian entry of row 3+r, column col of [A B] (FBDynamics_par.c operation order).
 __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const real* u,
                                               const real* p, const real* s, real dt) {
@@ -525,7 +801,8 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
   real luu[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) luu[c] = 2 * dt * sp.cw.fR[m][c];
-  const real dg2 = xl ? 2 * (w2 + rc.reg) : real(0.0);  // lxx + reg, see sweep_wb
+  // lxx + reg, see sweep_wb (two-row layout: both rows run this phase, row A adds)
+  const real dg2 = xl && rc.rp == 0 ? 2 * (w2 + rc.reg) : real(0.0);
   // rows 3, 4 of W do not depend on the knot
   const real zx[2] = {0, 0}, zu[4] = {0, 0, 0, 0};
   const real W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
@@ -643,7 +920,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
     for (int j = 0; j < 6; ++j) H[j] = Hn[j];
     Gv = Gn;
     const bool ok = gate && psd;
-    pend.ok = ok;
+    pend.ok = ok && rc.rp == 0;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -673,12 +950,11 @@ template <int NX>
 __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const ProbState* st,
                                RowLds& rl, const RowCtx& rc, int p) {
   constexpr bool wb = NX == 14;
-  const int t = rc.t;
   const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
   const real pos = d.refpos[(size_t)rc.b * sp.NK + ko + N - 1];
   const real* xe = traj_ptr(sp, d, rc.b, rc.nom, ko + N - 1);
   const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
-  if (al && t == 0) {
+  if (al && rc.lt == 0) {
     real hx[14], Hs[3][3], h;
     if (mode == 2) wb_touchdown_compact<kFront>(xe, &h, hx, Hs);
     else wb_touchdown_compact<kBack>(xe, &h, hx, Hs);
@@ -695,7 +971,7 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const Pr
   real* Gout = d.G + ((size_t)rc.b * sp.NK + ko + N - 1) * 14;
   const bool gate = go(rc);
   #pragma unroll 1
-  for (int e = t; e < NX * NX + NX; e += 16) {
+  for (int e = rc.lt; e < NX * NX + NX; e += rc.nl) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
       real v = i == j ? (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) : real(0.0);
@@ -789,7 +1065,8 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl,
 // rc.dV the matching dVnext.
 // WB_CODE = false: SRB phases only (the SRB half of a split sweep), no whole-body code in the
 // kernel (its register allocation is the SRB knot's, so a partials wave fits beside it).
-template <bool WB_CODE>
+// RPP: rows per problem (2: the whole-body phases run sweep_wb2, SRB phases on both rows).
+template <bool WB_CODE, int RPP>
 __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState* st, RowLds& rl,
                              RowCtx& rc, int p_hi, int p_lo) {
   for (int p = p_hi; p >= p_lo; --p) {
@@ -805,14 +1082,19 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState*
       if constexpr (WB_CODE) {
         terminal_value<14>(sp, d, st, rl, rc, p);
         const int mode = sp.mode[p];
-        if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
-        else sweep_wb<false>(sp, d, st, rl, rc, p);
+        if (RPP == 2) {
+          if (mode == 1 || mode == 3) sweep_wb2<true>(sp, d, st, rl, rc, p);
+          else sweep_wb2<false>(sp, d, st, rl, rc, p);
+        } else {
+          if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
+          else sweep_wb<false>(sp, d, st, rl, rc, p);
+        }
       }
     } else {
       terminal_value<6>(sp, d, st, rl, rc, p);
       sweep_srb(sp, d, st, rl, rc, p);
     }
-    if (was_go && rc.t == 0) st->dV[p] = rc.dV;
+    if (was_go && rc.lt == 0) st->dV[p] = rc.dV;
     if (!any_go(rc)) break;
   }
 }
@@ -821,8 +1103,8 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState*
 __device__ void zero_value(RowLds& rl, RowCtx& rc) {
   __syncthreads();
   #pragma unroll 1
-  for (int e = rc.t; e < 16 * MP; e += 16) rl.M[e] = real(0.0);
-  rl.Gs[rc.t] = real(0.0);
+  for (int e = rc.lt; e < 16 * MP; e += rc.nl) rl.M[e] = real(0.0);
+  if (rc.lt < 16) rl.Gs[rc.lt] = real(0.0);
   rc.dV = acc(0.0);
   __syncthreads();
 }
@@ -834,26 +1116,32 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
 #define MHPC_BWS_SRB_WAVES 2
 #endif
 
-// RPW problems per wave (rows 0..RPW-1 of the wave; the others idle).
+// RPW problems per wave, RPP rows per problem (rows 0..RPW*RPP-1 of the wave; the others
+// idle).  RPP = 2 (RPW = 2): problem q on rows 2q, 2q+1 sharing one RowLds (sweep_wb2).
 //
 // PART 0: the whole sweep with its regularisation retries (MultiPhaseDDP.cpp:196-241).
 // PART 1: the SRB phases of the first attempt only, the value function at the WB boundary
 // saved to d.carry (this launch runs beside the partials, which it does not read).
 // PART 2: the WB phases of the first attempt (rows whose SRB part passed), then the same
 // retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
-template <int RPW, int PART>
+template <int RPW, int PART, int RPP>
 __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(SolveParams sp, DevBufs d,
                                                                     real update_reg) {
+  static_assert(RPP == 1 || (RPP == 2 && RPW == 2 && PART != 1), "row layout");
   __shared__ BwsLds sh;
   const int row = threadIdx.x >> 4;
+  const int q = RPP == 2 ? row >> 1 : row;  // problem slot of the row
   RowCtx rc;
   rc.t = threadIdx.x & 15;
-  const int b0 = blockIdx.x * RPW + row;
+  rc.rp = RPP == 2 ? row & 1 : 0;
+  rc.lt = rc.t + 16 * rc.rp;
+  rc.nl = 16 * RPP;
+  const int b0 = blockIdx.x * RPW + q;
   rc.b = b0 < sp.B ? b0 : sp.B - 1;
   ProbState* st = &d.st[rc.b];
-  rc.act = row < RPW && b0 < sp.B && st->active && st->ddp_active;
+  rc.act = q < RPW && b0 < sp.B && st->active && st->ddp_active;
   if (!__builtin_amdgcn_ballot_w64(rc.act)) return;
-  RowLds& rl = sh.r[row];
+  RowLds& rl = sh.r[q];
   rc.nom = st->nom_slot;
   rc.reg = st->reg;
   rc.kn = rc.kn_wb = rc.px_reads = 0;
@@ -868,7 +1156,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     sweeps += rc.live ? 1 : 0;
     if (PART == 1) {
       zero_value(rl, rc);
-      sweep_phases<false>(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
+      sweep_phases<false, 1>(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
       BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       if (rc.act) {
@@ -887,16 +1175,16 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       const BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       #pragma unroll 1
-      for (int e = rc.t; e < 36; e += 16) rl.M[(e / 6) * MP + e % 6] = c.H[e];
-      if (rc.t < 6) rl.Gs[rc.t] = c.G[rc.t];
+      for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
+      if (rc.lt < 6) rl.Gs[rc.lt] = c.G[rc.lt];
       __syncthreads();
       rc.failed = rc.live && c.ok == 0;
       rc.kn += rc.live ? c.knots : 0;
       rc.dV = st->dV[sp.n_wb];
-      sweep_phases<true>(sp, d, st, rl, rc, sp.n_wb - 1, 0);
+      sweep_phases<true, RPP>(sp, d, st, rl, rc, sp.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
-      sweep_phases<true>(sp, d, st, rl, rc, sp.P - 1, 0);
+      sweep_phases<true, RPP>(sp, d, st, rl, rc, sp.P - 1, 0);
     }
     pending = rc.live && rc.failed;
     if (pending) {
@@ -909,7 +1197,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     }
     if (!__builtin_amdgcn_ballot_w64(pending)) break;
   }
-  if (rc.act && rc.t == 0) {
+  if (rc.act && rc.lt == 0) {
     st->cnt[C_DDP]++;
     st->cnt[C_BWS] += sweeps;
     st->cnt[C_BWS_KNOTS] += rc.kn;
@@ -934,22 +1222,38 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
   }
 }
 
-// Launch shape: sp.var_bws (mhpc_set_kernel_variant) or, by default, four problems per wave
-// (one wave per block).  Two / one problems per wave run the same per-row code on fewer rows
-// (tests/test_gpu_variants.py checks them bit for bit).
+// Launch shape: sp.var_bws (mhpc_set_kernel_variant) or bws_auto_variant.  Two / one
+// problems per wave run the same per-row code on fewer rows; PAIRS2 runs the whole-body phases
+// on two rows per problem (tests/test_gpu_variants.py checks them all bit for bit).
 // part: 0 whole sweep, 1 / 2 its SRB / WB halves (bws_split).
+// Default shape: one row per problem (four per wave) fills the chip from about a thousand
+// problems; up to 2048 the two-row layout (half the whole-body knot per row) is faster.
+#ifndef MHPC_BWS_PAIRS_MAX_B
+#define MHPC_BWS_PAIRS_MAX_B 2048
+#endif
+int bws_auto_variant(int B) {
+  return B <= MHPC_BWS_PAIRS_MAX_B ? MHPC_VARIANT_BWS_PAIRS2 : MHPC_VARIANT_BWS_ROWS4;
+}
+
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, int part,
                       hipStream_t s) {
-  const int v = sp.var_bws ? sp.var_bws : MHPC_VARIANT_BWS_ROWS4;
-  const int rpw = v == MHPC_VARIANT_BWS_ROWS1 ? 1 : v == MHPC_VARIANT_BWS_ROWS2 ? 2 : 4;
+  const int v = sp.var_bws ? sp.var_bws : bws_auto_variant(sp.B);
+  const int rpw = v == MHPC_VARIANT_BWS_ROWS1 ? 1 : (v == MHPC_VARIANT_BWS_ROWS2 ||
+                                                     v == MHPC_VARIANT_BWS_PAIRS2) ? 2 : 4;
   const dim3 grid((sp.B + rpw - 1) / rpw);
+  const dim3 grid4((sp.B + 3) / 4);
 #define MHPC_LAUNCH_BWS(R)                                                                    \
   do {                                                                                        \
-    if (part == 1) hipLaunchKernelGGL((k_bws<R, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
-    else if (part == 2) hipLaunchKernelGGL((k_bws<R, 2>), grid, dim3(64), 0, s, sp, d, update_reg); \
-    else hipLaunchKernelGGL((k_bws<R, 0>), grid, dim3(64), 0, s, sp, d, update_reg);           \
+    if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    else if (part == 2) hipLaunchKernelGGL((k_bws<R, 2, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    else hipLaunchKernelGGL((k_bws<R, 0, 1>), grid, dim3(64), 0, s, sp, d, update_reg);           \
   } while (0)
-  if (rpw == 1) MHPC_LAUNCH_BWS(1);
+  if (v == MHPC_VARIANT_BWS_PAIRS2) {
+    // the SRB half keeps one row per problem (its knot is short; four problems per wave)
+    if (part == 1) hipLaunchKernelGGL((k_bws<4, 1, 1>), grid4, dim3(64), 0, s, sp, d, update_reg);
+    else if (part == 2) hipLaunchKernelGGL((k_bws<2, 2, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
+    else hipLaunchKernelGGL((k_bws<2, 0, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
+  } else if (rpw == 1) MHPC_LAUNCH_BWS(1);
   else if (rpw == 2) MHPC_LAUNCH_BWS(2);
   else MHPC_LAUNCH_BWS(4);
 #undef MHPC_LAUNCH_BWS

@@ -1033,7 +1033,7 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
   SolveParams& sp = h->sp;
   if (which == MHPC_VARIANT_BWS) {
-    if (variant < 0 || variant > MHPC_VARIANT_BWS_ROWS1) return fail(MHPC_ERR_INVALID, "no such backward-sweep variant");
+    if (variant < 0 || variant > MHPC_VARIANT_BWS_PAIRS2) return fail(MHPC_ERR_INVALID, "no such backward-sweep variant");
     sp.var_bws = variant;
     return MHPC_OK;
   }

@@ -1,16 +1,17 @@
 """Every launch variant of the backward sweep and of the line search, and the batch sizes at
 which the automatic choice switches between them, against the oracle and against each other.
 
-The launch shape is chosen from the batch size (k_bws 1-wave / 2-wave build, k_rollout pair /
-pipelined / fused, staged or not), so a problem's result must not depend on the
+The launch shape is chosen from the batch size (k_bws two rows per problem up to 2048 problems,
+one row per problem above; k_rollout pair / pipelined / fused, staged or not), so a problem's result must not depend on the
 batch it is solved in (per-problem outputs on G GPUs bitwise-identical to 1
 GPU).  Here:
   * every (bws, rollout) variant pinned through mhpc_set_kernel_variant at batch 256 (C3) and
     64 (C5, fp64 and fp32): bitwise identical to each other, and the fp64 ones within the
     solve tolerance of the oracle with an identical decision trace (MultiPhaseDDP.cpp:154-289);
-  * the north-star batch 4096 with the automatic choice (k_bws 2-wave, fused line search):
-    a spread sample of 64 problems (including the last, partial block) against the oracle, and
-    bitwise against the same initial states solved at batch 8 (1-wave, pair)."""
+  * the north-star batch 4096 with the automatic choice (k_bws one row per problem, fused
+    line search): a spread sample of 64 problems (including the last, partial block) against
+    the oracle, and bitwise against the same initial states solved at batch 8 (two rows per
+    problem, pair)."""
 import itertools
 
 import numpy as np
@@ -61,12 +62,12 @@ def assert_oracle(got, ref, tol=SOLVE_TOL):
 
 
 ALL_VARIANTS = [(b, r, "auto") for b, r in
-                itertools.product(("rows4", "rows2", "rows1"),
+                itertools.product(("rows4", "rows2", "rows1", "pairs2"),
                                   ("pair", "pipe_staged", "pipe", "fused_staged", "fused"))]
 # the backward sweep as one launch after the partials (the default splits it into an SRB
 # launch beside the partials and a WB launch after them)
 ALL_VARIANTS += [("rows4", "pair", "off"), ("rows2", "fused", "off"), ("rows1", "pipe", "off"),
-                 ("auto", "auto", "off")]
+                 ("pairs2", "fused_staged", "off"), ("auto", "auto", "off")]
 
 
 def test_variant_rejected_when_it_does_not_apply(need_gpu):
@@ -81,7 +82,7 @@ def test_variant_rejected_when_it_does_not_apply(need_gpu):
         loco.set_kernel_variant(bws="rows2", rollout="fused")
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 7, 0) == capi.MHPC_ERR_INVALID
         assert capi.lib().mhpc_set_kernel_variant(loco._h, 2, 3) == capi.MHPC_ERR_INVALID
-        assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 4) == capi.MHPC_ERR_INVALID
+        assert capi.lib().mhpc_set_kernel_variant(loco._h, 0, 5) == capi.MHPC_ERR_INVALID
         assert capi.lib().mhpc_set_kernel_variant(loco._h, capi.MHPC_VARIANT_SUBBATCH,
                                                   capi.MHPC_MAX_SUBBATCH + 1) == capi.MHPC_ERR_INVALID
     finally:

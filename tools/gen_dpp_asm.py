@@ -134,6 +134,24 @@ def blocks():
     for c in (7, 8):
         B.append(lane_block(f"sb_even7_{c}", even7, c, ["s", "m"],
                             f"acc a += sum_r bcast(s[a], 2r) * m[r], r < 7, {c} accumulators"))
+    # ---- whole body, two rows per problem (sweep_wb2): row A holds the configuration
+    # columns 0..6, row B the velocity columns 7..13 in the same slots (its broadcast set puts
+    # column 7 + s on lane 2 s), both the control columns 14..17 ----
+    terms = []
+    for j in range(7):
+        rnd = [(f"wb[{j}]", f"h[{j}]", 12), (f"wb[{j}]", f"h[{j}]", 14), (f"wb[{j}]", f"h[{j}]", 15),
+               (f"w2[{j}]", f"h[{j}]", 14), (f"w2[{j}]", f"h[{j}]", 15)]
+        terms.append(rnd)
+    B.append(Block("wb2_s_b", 5, ["wb", "w2", "h"], terms,
+                   "two-row S = H [A B], slots 6..10 (column 6 / 13, 14, 15, 16, 17)"))
+    terms = []
+    for j in range(2):
+        rnd = [(f"g[{j}]", f"cc[{j}]", 12), (f"g[{j}]", f"cc[{j}]", 14), (f"g[{j}]", f"cc[{j}]", 15),
+               (f"g2[{j}]", f"cc[{j}]", 14), (f"g2[{j}]", f"cc[{j}]", 15),
+               (f"g2[{j}]", f"cc2[{j}]", 14), (f"g2[{j}]", f"cc2[{j}]", 15)]
+        terms.append(rnd)
+    B.append(Block("wb2_st_b", 7, ["g", "g2", "cc", "cc2"], terms,
+                   "two-row stance terms, slots 6..10 and the control rows 2, 3"))
     # ---- SRB (NQ = 3) ----
     for nm, cols in (("a", range(0, 5)), ("b", range(5, 10))):
         B.append(col_block(f"srb_s_{nm}", 3, list(cols), 3, ["w", "h"],
