@@ -1060,6 +1060,18 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl,
   __syncthreads();
 }
 
+// Optional cycle accounting of the sweep (build with -DMHPC_BWS_TIMING, read with
+// mhpc_dbg_bws_cycles, tools/bws_timing.py; lane 0 of every wave): 0 / 1 WB knot loops and
+// knots, 2 / 3 SRB knot loops and knots, 4 terminal values, 5 impact steps, 6 kernel, 7 waves.
+#ifdef MHPC_BWS_TIMING
+__device__ unsigned long long g_bws_cyc[8];
+#define BWS_T(v) const unsigned long long v = threadIdx.x == 0 ? clock64() : 0ull
+#define BWS_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_bws_cyc[i], (unsigned long long)(v)); } while (0)
+#else
+#define BWS_T(v) do { } while (0)
+#define BWS_ADD(i, v) do { } while (0)
+#endif
+
 // One sweep attempt over phases p_hi..p_lo (MultiPhaseDDP::backward_sweep).  On entry
 // rl.M / rl.Gs hold the value function entering phase p_hi (zero for the last phase) and
 // rc.dV the matching dVnext.
@@ -1074,13 +1086,18 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState*
     const bool was_go = go(rc);
     if (p + 1 < sp.P) {
       if constexpr (WB_CODE) {
+        BWS_T(ti0);
         if (wb) impact_step(sp, d, rl, rc, p);
+        BWS_ADD(5, clock64() - ti0);
       }
       if (was_go) rc.dV = st->dV[p + 1];  // dVnext
     }
+    BWS_T(tt0);
     if (wb) {
       if constexpr (WB_CODE) {
         terminal_value<14>(sp, d, st, rl, rc, p);
+        BWS_ADD(4, clock64() - tt0);
+        BWS_T(tw0);
         const int mode = sp.mode[p];
         if (RPP == 2) {
           if (mode == 1 || mode == 3) sweep_wb2<true>(sp, d, st, rl, rc, p);
@@ -1089,10 +1106,16 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState*
           if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
           else sweep_wb<false>(sp, d, st, rl, rc, p);
         }
+        BWS_ADD(0, clock64() - tw0);
+        BWS_ADD(1, sp.N[p] - 1);
       }
     } else {
       terminal_value<6>(sp, d, st, rl, rc, p);
+      BWS_ADD(4, clock64() - tt0);
+      BWS_T(ts0);
       sweep_srb(sp, d, st, rl, rc, p);
+      BWS_ADD(2, clock64() - ts0);
+      BWS_ADD(3, sp.N[p] - 1);
     }
     if (was_go && rc.lt == 0) st->dV[p] = rc.dV;
     if (!any_go(rc)) break;
@@ -1129,6 +1152,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
                                                                     real update_reg) {
   static_assert(RPP == 1 || (RPP == 2 && RPW == 2 && PART != 1), "row layout");
   __shared__ BwsLds sh;
+  BWS_T(tk0);
   const int row = threadIdx.x >> 4;
   const int q = RPP == 2 ? row >> 1 : row;  // problem slot of the row
   RowCtx rc;
@@ -1197,6 +1221,8 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     }
     if (!__builtin_amdgcn_ballot_w64(pending)) break;
   }
+  BWS_ADD(6, clock64() - tk0);
+  BWS_ADD(7, 1);
   if (rc.act && rc.lt == 0) {
     st->cnt[C_DDP]++;
     st->cnt[C_BWS] += sweeps;
@@ -1267,3 +1293,17 @@ bool bws_split(const SolveParams& sp) {
 }
 
 }  // namespace MHPC_NS
+
+#ifdef MHPC_BWS_TIMING
+extern "C" int mhpc_dbg_bws_cycles(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_bws_cyc), sizeof(unsigned long long) * 8) !=
+      hipSuccess)
+    return 1;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

@@ -255,6 +255,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
   auto store_rec = [&](const real* r, int n, int kk) __attribute__((always_inline)) {
+#ifdef MHPC_RO_NOSTORE  // timing experiment only: results are wrong
+    if (kk >= 0) return;
+#endif
     real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
     for (int i = 0; i < RING_W / 2; ++i)

@@ -73,8 +73,10 @@ def main():
     # blocks of the loop: from the header to the last block that names it, plus nested ones
     keys = list(bl)
     hdr = hdr if hdr in keys else ".L" + hdr
-    i0 = keys.index(hdr)
-    i1 = max(i for i, k in enumerate(keys) if bl[k]["loop"] and ".L" + bl[k]["loop"][0] in (hdr, ".L" + hdr))
+    # every block whose innermost loop is this one (the layout may rotate the header to the
+    # end), plus the blocks laid out between the header and the last such block (nested loops)
+    member = [i for i, k in enumerate(keys) if bl[k]["loop"] and ".L" + bl[k]["loop"][0] in (hdr, ".L" + hdr)]
+    i0, i1 = min(member), max(member)
     tot = collections.Counter()
     ops = collections.Counter()
     for k in keys[i0:i1 + 1]:
