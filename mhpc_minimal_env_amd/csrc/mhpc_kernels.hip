@@ -255,8 +255,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
   auto store_rec = [&](const real* r, int n, int kk) __attribute__((always_inline)) {
-#ifdef MHPC_RO_NOSTORE  // timing experiment only: results are wrong
+#ifdef MHPC_RO_NOSTORE  // timing experiments only: results are wrong
+#if MHPC_RO_NOSTORE == 1
     if (kk >= 0) return;
+#else
+    n = n < 2 * MHPC_RO_NOSTORE ? n : 2 * MHPC_RO_NOSTORE;  // the first pieces only
+#endif
 #endif
     real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
@@ -422,8 +426,19 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // cost side, phase constants: ReB parameters and the staged position references
   struct CostPhase {
     real delta, etq, egr, refT;
-    bool sref;
-    const real* refpos;
+    const __attribute__((address_space(1))) real* refpos;  // global (not a flat pointer)
+  };
+  // Position references of phase (N, ko) into the LDS stage (cost side: one wave writes and
+  // reads them).  The staged variants read every knot's reference from LDS and run only when
+  // every phase fits the stage (launch_rollout): a global load in the cost loop would be a
+  // VM-counter wait, and on gfx950's single in-order counter that wait also covers every
+  // record store issued before it -- which was most of the stores' cost in the line search.
+  auto stage_ref = [&](int N, int ko) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
+      const int fi = lane + 64 * i, rl = fi / ST_RMAX, rk = fi - rl * ST_RMAX;
+      if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
+    }
   };
   auto cost_phase_begin = [&](int p) __attribute__((always_inline)) {
     CostPhase c;
@@ -431,18 +446,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const bool wb = p < sp.n_wb;
     c.delta = c.etq = c.egr = real(0.0);
     if (run && wb) { c.delta = st->delta[p]; c.etq = st->eps_tq[p]; c.egr = st->eps_grf[p]; }
-    c.refpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
-    // position references of the phase: staged in LDS by the cost side (one round trip per
-    // phase), read from HBM per knot when the phase is longer than the stage
-    c.sref = ST && N <= ST_RMAX;
-    if (c.sref) {
-#pragma unroll
-      for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
-        const int fi = lane + 64 * i, rl = fi / ST_RMAX, rk = fi - rl * ST_RMAX;
-        if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
-      }
-    }
-    c.refT = run ? (c.sref ? sRef[lp][N - 1] : c.refpos[N - 1]) : real(0.0);
+    c.refpos = (const __attribute__((address_space(1))) real*)(d.refpos + (size_t)(in ? b : 0) * sp.NK + ko);
+    c.refT = run ? c.refpos[N - 1] : real(0.0);
+    if (ST) stage_ref(N, ko);
     return c;
   };
   // cost side: the running cost of knot kk from record r (knot order: the serial rollout's
@@ -452,7 +458,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const int mode = sp.mode[p], ko = sp.ko[p];
     const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
-    const real pos = c.sref ? sRef[lp][kk] : c.refpos[kk];
+    const real pos = ST ? sRef[lp][kk] : c.refpos[kk];
     V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, c.delta, c.etq, c.egr)
             : fb_running_cost(sp, mode, dt, pos, r, r + 6);
     store_rec(r, wb ? RING_W : 14, ko + kk);
@@ -1522,7 +1528,10 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
                                 // wave per block only competes for issue slots
 #endif
-  bool st = ppw <= ST_PPW;
+  // staged: ST_PPW problems per wave at most, and every phase within the reference stage
+  bool fits = true;
+  for (int p = 0; p < sp.P; ++p) fits = fits && sp.N[p] <= ST_RMAX;
+  bool st = ppw <= ST_PPW && fits;
   // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
   const int ppw2 = std::min(32 / sp.n_cand, RO_PAIR_PPB);
   const int nblk2 = ppw2 > 0 ? (sp.B + ppw2 - 1) / ppw2 : 0;
@@ -1537,6 +1546,7 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
     pair = v == MHPC_VARIANT_RO_PAIR;
     pipe = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_PIPE;
     st = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_FUSED_STAGED;
+    if (!fits) pair = st = false;  // a phase longer than the stage: the unstaged form
   }
   if (pair)
     hipLaunchKernelGGL((k_rollout<true, true, true>), dim3(nblk2), dim3(128), 0, s, sp, d, al_iter,
