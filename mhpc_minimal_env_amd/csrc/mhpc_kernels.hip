@@ -265,7 +265,14 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
     for (int i = 0; i < RING_W / 2; ++i)
-      if (2 * i < n) o[i] = real2{r[2 * i], r[2 * i + 1]};
+      if (2 * i < n) {
+#ifdef MHPC_RO_NT_STORE  // experiment: streaming (non-temporal) record stores
+        typedef real v2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(v2{r[2 * i], r[2 * i + 1]}, reinterpret_cast<v2*>(o + i));
+#else
+        o[i] = real2{r[2 * i], r[2 * i + 1]};
+#endif
+      }
   };
   const int b0 = blockIdx.x * ppw;
   real f[4] = {0, 0, 0, 0}, sc[2] = {0, 0};  // SRB phase: foothold, contact flags

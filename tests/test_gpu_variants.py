@@ -115,6 +115,27 @@ def test_c5_every_variant_bitwise(need_gpu, precision):
                        f"C5/{precision} bws={bws} rollout={ro} overlap={ov}")
 
 
+def test_long_phases_unstaged_line_search(need_gpu):
+    """Phases longer than the line search's LDS reference stage (ST_RMAX = 128 knots) run the
+    unstaged kernels, also when a staged variant is pinned (launch_rollout): the same results
+    bit for bit, and the oracle's."""
+    from mhpc_minimal_env_amd import locomotion as L
+    desc = L.make_problem_desc(2, 2, [1, 2, 3, 4], [0.15] * 4, 0.001, 0.001, 1.5)
+    assert min(desc.N[p] for p in range(4)) > 128
+    x0 = configs_x0(desc, 12, offset=4242)
+    base = solve(desc, x0)
+    O = _oracle()
+    if O is not None:
+        assert_oracle(base, O.solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=8))
+    for ro in ("pair", "fused_staged", "pipe", "fused"):
+        assert_bitwise(solve(desc, x0, rollout=ro), base, f"long phases, rollout={ro}")
+
+
+def configs_x0(desc, B, offset):
+    from mhpc_minimal_env_amd import configs
+    return configs.x0_for(desc, B, offset=offset)
+
+
 @pytest.mark.parametrize("name,precision", [("c3", 64), ("c5", 32)])
 def test_sub_batches_bitwise(need_gpu, name, precision):
     """The batch as 2..4 concurrently scheduled sub-batches (own stream pairs, staggered,
