@@ -262,6 +262,11 @@ void mhpc_destroy(mhpc_handle* h);
                                          so that one block's line search shares the chip with
                                          another block's sweep); 0 = automatic */
 #define MHPC_MAX_SUBBATCH 4
+#define MHPC_VARIANT_RO_STORE 4       /* which: line-search trials that store their knot
+                                         records: the first `variant` (1..32) and the last;
+                                         an accepted trial without records is rolled out again
+                                         into its slot (same arithmetic, bit for bit);
+                                         0 = the default (4) */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

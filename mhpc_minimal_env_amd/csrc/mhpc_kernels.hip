@@ -60,6 +60,20 @@ __device__ __forceinline__ real fb_dot(const real* Kr, const real* x, const real
   return fb;
 }
 
+// Line-search trials whose running knot records are stored (j < RO_STORE_FIRST, and the last
+// trial, which the reference adopts when none is accepted); every trial stores its terminal
+// states.  The Armijo test accepts an early trial almost always (CPU oracle, C3 x512: trial
+// 1-4 or none; C5 x128: trial 2-5), and the record stores are a large part of a launch
+// (MHPC_RO_STORE_FIRST=4 A/B: -25 % k_rollout per launch at batch 4096, -4 % at 1024).  An
+// accepted trial without records is rolled out again into its slot right after the line
+// search (k_rollout mode 2, same arithmetic: bit for bit).  The handle's sp.ro_store
+// (mhpc_set_kernel_variant(MHPC_VARIANT_RO_STORE)) overrides it.
+#ifndef MHPC_RO_STORE_FIRST
+#define MHPC_RO_STORE_FIRST 4
+#endif
+constexpr int RO_STORE_FIRST = MHPC_RO_STORE_FIRST;
+int ro_store_default() { return RO_STORE_FIRST; }
+
 // Problems per block of the pair variant (at most 32 / n_cand = 3 with 10 candidates).
 #ifndef MHPC_RO_PAIR_PPB
 #define MHPC_RO_PAIR_PPB 3
@@ -180,6 +194,9 @@ __device__ unsigned long long g_ro_cyc[11];
 // full = 1: forward_sweep(0) as a real rollout (one lane per problem, eps = 0, always
 // adopted) -- needed when the nominal is not a rollout of its own controls from x0, i.e.
 // after mhpc_update_problem (receding horizon); otherwise k_cost replaces it.
+// full = 2: the line search's accepted trial again (eps of st->reroll_j from the nominal the
+// line search started from, into the new nominal slot), records only, for the problems whose
+// trial stored none (RO_STORE_FIRST).
 // ST = true: the line search reads nominal / gains / references through the LDS stage
 // (requires n_cand >= 10, i.e. <= ST_PPW problems per wave).
 // PAIR (with PIPE and ST): the dynamics wave gives each candidate a lane pair (even lane
@@ -225,9 +242,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   ProbState* st = nullptr;
   if (in) {
     st = &d.st[b];
-    run = st->active && (full || st->ddp_active);
-    nom = st->nom_slot;
-    slot = j < nom ? j : j + 1;
+    if (full == 2) {  // re-roll of the accepted trial into the new nominal slot
+      run = st->active && st->reroll_j >= 0;
+      nom = st->reroll_nom;
+      slot = st->nom_slot;
+    } else {
+      run = st->active && (full || st->ddp_active);
+      nom = st->nom_slot;
+      slot = j < nom ? j : j + 1;
+    }
   }
   if (w0 && run) sAny = 1;
   if (ST && w0 && run && j == 0) sNom[lp] = nom;
@@ -236,7 +259,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 #pragma unroll
   for (int i = 0; i < ST_PPW; ++i) nomv[i] = ST ? __builtin_amdgcn_readfirstlane(sNom[i]) : -1;
   if (!sAny) return;  // uniform: no problem of this block is still iterating
-  if (full && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
+  if (full == 1 && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
     if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
     const bool reb_off = (st->viol > real(0.05)) || al_iter == 1;
     st->reb_active = (st->cap_reb && !reb_off) ? 1 : 0;
@@ -244,7 +267,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   }
   if (full) __syncthreads();
 
-  const real eps = run && !full ? sp.eps[j] : real(0.0);
+  const real eps = !run ? real(0.0) : full == 2 ? sp.eps[st->reroll_j] : !full ? sp.eps[j] : real(0.0);
   const bool reb = run && st->reb_active;
   real x[14];
   if (w0 && run) {
@@ -254,7 +277,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   acc J = 0, viol2 = 0;
   // wave 1: store the lane's ring record (n reals, n even) to knot kk of its slot with
   // 2-wide stores (records are aligned to them: KS * sizeof(real))
-  auto store_rec = [&](const real* r, int n, int kk) __attribute__((always_inline)) {
+  auto store_rec = [&](const real* r, int n, int kk, bool running) __attribute__((always_inline)) {
 #ifdef MHPC_RO_NOSTORE  // timing experiments only: results are wrong
 #if MHPC_RO_NOSTORE == 1
     if (kk >= 0) return;
@@ -262,17 +285,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     n = n < 2 * MHPC_RO_NOSTORE ? n : 2 * MHPC_RO_NOSTORE;  // the first pieces only
 #endif
 #endif
+    if (running && !full && j >= sp.ro_store && j != nc - 1) return;  // see RO_STORE_FIRST
     real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, kk));
 #pragma unroll
     for (int i = 0; i < RING_W / 2; ++i)
-      if (2 * i < n) {
-#ifdef MHPC_RO_NT_STORE  // experiment: streaming (non-temporal) record stores
-        typedef real v2 __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(v2{r[2 * i], r[2 * i + 1]}, reinterpret_cast<v2*>(o + i));
-#else
-        o[i] = real2{r[2 * i], r[2 * i + 1]};
-#endif
-      }
+      if (2 * i < n) o[i] = real2{r[2 * i], r[2 * i + 1]};
   };
   const int b0 = blockIdx.x * ppw;
   real f[4] = {0, 0, 0, 0}, sc[2] = {0, 0};  // SRB phase: foothold, contact flags
@@ -466,9 +483,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const real dt = sp.dt[p];
     const bool wb = p < sp.n_wb;
     const real pos = ST ? sRef[lp][kk] : c.refpos[kk];
-    V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, c.delta, c.etq, c.egr)
-            : fb_running_cost(sp, mode, dt, pos, r, r + 6);
-    store_rec(r, wb ? RING_W : 14, ko + kk);
+    if (full != 2)  // (a re-roll only writes the records)
+      V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, c.delta, c.etq, c.egr)
+              : fb_running_cost(sp, mode, dt, pos, r, r + 6);
+    store_rec(r, wb ? RING_W : 14, ko + kk, true);
   };
   auto ring_rec = [&](int sl, real* r, int n) __attribute__((always_inline)) {
 #pragma unroll
@@ -480,6 +498,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     MHPC_NO_FMA_COST
     const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
     const bool wb = p < sp.n_wb;
+    if (full == 2) {
+      store_rec(xe, wb ? 14 : 6, ko + N - 1, false);
+      return;
+    }
     real h = 0;
     if (wb) {
       real rx[14];
@@ -507,7 +529,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     viol2 += acc(h) * h;
     sV[p][lane] = V;
     sH[p][lane] = h;
-    store_rec(xe, wb ? 14 : 6, ko + N - 1);
+    store_rec(xe, wb ? 14 : 6, ko + N - 1, false);
   };
 
   if constexpr (PIPE) {
@@ -690,6 +712,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   if (lane == 0)
     for (int i = 0; i < 11; ++i) atomicAdd(&g_ro_cyc[i], ro_cyc[i]);
 #endif
+  if (full == 2) {
+    if (w1 && run) st->reroll_j = -1;
+    return;
+  }
   if (full) {
     if (w1 && run) {
       st->J = J;
@@ -718,6 +744,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       if (sJ[lane + c] <= rhs) { sel = c; nls = c + 1; break; }
     }
     const int sl = lane + sel;
+    st->reroll_j = (sel >= sp.ro_store && sel != nc - 1) ? sel : -1;
+    st->reroll_nom = nom;
     st->J = sJ[sl];
     st->viol = sViol[sl];
     for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][sl]; st->h[p] = sH[p][sl]; }
@@ -1154,6 +1182,8 @@ __device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int
   st->par_al = 0;
   st->ls_nt = 0;
   st->ls_nom = 0;
+  st->reroll_j = -1;
+  st->reroll_nom = 0;
   for (int p = 0; p < MAXP; ++p) {
     st->par_sigma[p] = 0; st->par_lambda[p] = 0; st->ls_sigma[p] = 0; st->ls_lambda[p] = 0;
   }
@@ -1570,6 +1600,11 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   else
     hipLaunchKernelGGL((k_rollout<false, false, false>), dim3(nblk), dim3(64), 0, s, sp, d,
                        al_iter, ddp_iter, max_ddp, 0);
+  // the accepted trials whose records were not stored (RO_STORE_FIRST), rolled out again
+  // (lane = problem; a block without one returns at once)
+  if (sp.ro_store < sp.n_cand - 1)
+    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
+                       sp, d, al_iter, 0, 0, 2);
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,

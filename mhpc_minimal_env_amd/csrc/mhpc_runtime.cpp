@@ -21,6 +21,7 @@ hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int
 hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
 bool bws_split(const SolveParams&);
+int ro_store_default();
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, hipStream_t);
@@ -358,6 +359,7 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
     sp.eps[nc++] = eps;
   }
   sp.n_cand = nc;
+  sp.ro_store = ro_store_default();
   sp.nslot = nc + 1;
   sp.gamma = opt->gamma;
   sp.DDP_thresh = opt->DDP_thresh;
@@ -1040,6 +1042,11 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
   if (which == MHPC_VARIANT_OVERLAP) {
     if (variant < 0 || variant > MHPC_VARIANT_OVERLAP_OFF) return fail(MHPC_ERR_INVALID, "no such overlap variant");
     sp.var_overlap = variant;
+    return MHPC_OK;
+  }
+  if (which == MHPC_VARIANT_RO_STORE) {
+    if (variant < 0 || variant > MAXC) return fail(MHPC_ERR_INVALID, "stored trials must be 0..32");
+    sp.ro_store = variant ? variant : ro_store_default();
     return MHPC_OK;
   }
   if (which == MHPC_VARIANT_SUBBATCH) {

@@ -69,6 +69,9 @@ struct SolveParams {
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
   int ncu, var_bws, var_ro, var_overlap;
+  // line-search trials that store their running knot records (the first ro_store, and the
+  // last; the rest are rolled out again when accepted -- mhpc_kernels.hip RO_STORE_FIRST)
+  int ro_store;
   // cost weights (diagonals per mode, CostBase.h:9-46 / MHPCCost.cpp:24-75) and constraint
   // parameters (ConstraintsBase.h:11-50 / MHPCConstraints.cpp:14-88): mhpc_set_cost_weights /
   // mhpc_set_constraint_params; read by every kernel from its parameter block
@@ -109,6 +112,10 @@ struct ProbState {
   // j < ls_nom ? j : j + 1.
   int32_t ls_nt, ls_nom;
   real ls_sigma[MAXP], ls_lambda[MAXP];
+  // line-search trial whose running records were not stored (trials j >= RO_STORE_FIRST but
+  // the last, mhpc_kernels.hip) and must be rolled out again into its slot, -1 if none; the
+  // nominal slot that line search started from
+  int32_t reroll_j, reroll_nom;
   // MultiPhaseDDP::_option as solve() leaves it: ReB_active and update_penalty are rewritten
   // inside the AL loop (MultiPhaseDDP.cpp:178-183, 273-277) and the next solve() starts from
   // the rewritten values (captured at its first AL iteration: cap_*) -- visible across the

@@ -430,12 +430,15 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
     def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto",
-                           sub_batches: int = 0):
+                           sub_batches: int = 0, ro_store: int = 0):
         """Pin the backward-sweep / line-search launch variant, the partials / sweep
-        overlap and the number of concurrently scheduled sub-batches
-        (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS / capi.RO_VARIANTS /
-        capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by batch size and phase layout."""
+        overlap, the number of concurrently scheduled sub-batches and the number of
+        line-search trials that store their knot records (mhpc_set_kernel_variant); names in
+        capi.BWS_VARIANTS / capi.RO_VARIANTS / capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by
+        batch size and phase layout (ro_store 0: the default)."""
         L = capi.lib()
+        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO_STORE, int(ro_store)),
+                   "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SUBBATCH, int(sub_batches)),
                    "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_OVERLAP,
