@@ -267,7 +267,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   }
   if (full) __syncthreads();
 
-  const real eps = !run ? real(0.0) : full == 2 ? sp.eps[st->reroll_j] : !full ? sp.eps[j] : real(0.0);
+  // (mode 2 reads its step size from the state: a per-lane index into the parameter block
+  // here made the compiler copy the whole block to scratch)
+  const real eps = run && !full ? sp.eps[j] : run && full == 2 ? st->reroll_eps : real(0.0);
   const bool reb = run && st->reb_active;
   real x[14];
   if (w0 && run) {
@@ -746,6 +748,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const int sl = lane + sel;
     st->reroll_j = (sel >= sp.ro_store && sel != nc - 1) ? sel : -1;
     st->reroll_nom = nom;
+    st->reroll_eps = sp.eps[sel];
     st->J = sJ[sl];
     st->viol = sViol[sl];
     for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][sl]; st->h[p] = sH[p][sl]; }
@@ -1184,6 +1187,7 @@ __device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int
   st->ls_nom = 0;
   st->reroll_j = -1;
   st->reroll_nom = 0;
+  st->reroll_eps = real(0.0);
   for (int p = 0; p < MAXP; ++p) {
     st->par_sigma[p] = 0; st->par_lambda[p] = 0; st->ls_sigma[p] = 0; st->ls_lambda[p] = 0;
   }

@@ -116,6 +116,7 @@ struct ProbState {
   // the last, mhpc_kernels.hip) and must be rolled out again into its slot, -1 if none; the
   // nominal slot that line search started from
   int32_t reroll_j, reroll_nom;
+  real reroll_eps;  // its step size (eps of trial reroll_j)
   // MultiPhaseDDP::_option as solve() leaves it: ReB_active and update_penalty are rewritten
   // inside the AL loop (MultiPhaseDDP.cpp:178-183, 273-277) and the next solve() starts from
   // the rewritten values (captured at its first AL iteration: cap_*) -- visible across the

@@ -437,8 +437,10 @@ class MHPCLocomotion:
         capi.BWS_VARIANTS / capi.RO_VARIANTS / capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by
         batch size and phase layout (ro_store 0: the default)."""
         L = capi.lib()
-        capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO_STORE, int(ro_store)),
-                   "mhpc_set_kernel_variant")
+        if ro_store or getattr(self, "_ro_store_pinned", False):
+            capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO_STORE, int(ro_store)),
+                       "mhpc_set_kernel_variant")
+            self._ro_store_pinned = bool(ro_store)
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SUBBATCH, int(sub_batches)),
                    "mhpc_set_kernel_variant")
         capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_OVERLAP,
