@@ -1625,12 +1625,23 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real
                      phix);
   return hipGetLastError();
 }
-hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
+// The direction groups write disjoint columns of the records: with a second stream s3 the
+// velocity / control group (G = 1, 252 VGPRs, two waves per SIMD) runs beside the
+// configuration group (340 VGPRs, one wave per SIMD) and fills the SIMDs its tail leaves;
+// s joins s3 before returning.
+hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s, hipStream_t s3,
+                           hipEvent_t fork, hipEvent_t join) {
   const long tk = (long)sp.B * sp.par_knots, ti = (long)sp.B * sp.par_imp;
+  const bool two = s3 && fork && join && kParGroups == 2 && tk > 0;
+  if (two) {
+    hipError_t e = hipEventRecord(fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s3, fork, 0);
+    if (e != hipSuccess) return e;
+  }
   if (tk > 0) {
     const dim3 grid((unsigned)((tk + 255) / 256));
+    hipLaunchKernelGGL(k_partials<1>, grid, dim3(256), 0, two ? s3 : s, sp, d);
     hipLaunchKernelGGL(k_partials<0>, grid, dim3(256), 0, s, sp, d);
-    hipLaunchKernelGGL(k_partials<1>, grid, dim3(256), 0, s, sp, d);
     if (kParGroups == 4) {
       hipLaunchKernelGGL(k_partials<2>, grid, dim3(256), 0, s, sp, d);
       hipLaunchKernelGGL(k_partials<3>, grid, dim3(256), 0, s, sp, d);
@@ -1638,6 +1649,11 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   }
   if (ti > 0)
     hipLaunchKernelGGL(k_partials_impact, dim3((unsigned)((ti + 255) / 256)), dim3(256), 0, s, sp, d);
+  if (two) {
+    hipError_t e = hipEventRecord(join, s3);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+    if (e != hipSuccess) return e;
+  }
   return hipGetLastError();
 }
 hipError_t launch_al_end(const SolveParams& sp, const DevBufs& d, int last, hipStream_t s) {

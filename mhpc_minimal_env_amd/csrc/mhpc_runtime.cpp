@@ -18,7 +18,8 @@ namespace MHPC_NS {
 hipError_t launch_init(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_reset_arrays(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_rollout(const SolveParams&, const DevBufs&, int, int, int, int, hipStream_t);
-hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t);
+hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t, hipStream_t, hipEvent_t,
+                           hipEvent_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
 bool bws_split(const SolveParams&);
 int ro_store_default();
@@ -81,8 +82,8 @@ struct Handle {
   hipStream_t stream = nullptr;
   // second stream: the partials run there beside the SRB half of the backward sweep
   // (fork / join events order it against the main stream)
-  hipStream_t stream2 = nullptr;
-  hipEvent_t evfork = nullptr, evjoin = nullptr;
+  hipStream_t stream2 = nullptr, stream3 = nullptr;  // stream3: the partials' second group
+  hipEvent_t evfork = nullptr, evjoin = nullptr, evpfork = nullptr, evpjoin = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool x0_set = false, initialized = false, solved = false, x0_changed = false;
   // constraint parameters replaced after the last initialize / update_problem: their AL / ReB
@@ -113,8 +114,9 @@ struct Handle {
   // problems, each block on its own stream pair; created on first use
   int nsub_req = 0;
   struct SubStreams {
-    hipStream_t s1 = nullptr, s2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, gate = nullptr, done = nullptr;
+    hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // s3: the partials' second group
+    hipEvent_t fork = nullptr, join = nullptr, gate = nullptr, done = nullptr, pfork = nullptr,
+               pjoin = nullptr;
   };
   std::vector<SubStreams> subs;
   hipEvent_t evstart = nullptr;
@@ -407,6 +409,9 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evfork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evjoin, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evpfork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evpjoin, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
   // zero x0 on the handle's own (non-blocking) stream: a null-stream memset would not be
@@ -548,8 +553,8 @@ struct SolveOp {
 struct SolveBlock {
   SolveParams sp;
   DevBufs d;
-  hipStream_t s1, s2;
-  hipEvent_t fork, join;
+  hipStream_t s1, s2, s3;
+  hipEvent_t fork, join, pfork, pjoin;
 };
 
 // Problems [b0, b0 + sp.B) of the handle's arrays as the kernels index them (b * per-problem
@@ -609,12 +614,12 @@ static int issue_op(Handle* h, const SolveBlock& k, const SolveOp& op) {
       break;
     case OP_PAR:
       if (!split) {
-        LAUNCH_ON(h, K_PAR, k.s1, launch_partials(sp, d, k.s1));
+        LAUNCH_ON(h, K_PAR, k.s1, launch_partials(sp, d, k.s1, k.s3, k.pfork, k.pjoin));
         break;
       }
       HIPCHK(hipEventRecord(k.fork, k.s1));
       HIPCHK(hipStreamWaitEvent(k.s2, k.fork, 0));
-      LAUNCH_ON(h, K_PAR, k.s2, launch_partials(sp, d, k.s2));
+      LAUNCH_ON(h, K_PAR, k.s2, launch_partials(sp, d, k.s2, k.s3, k.pfork, k.pjoin));
       HIPCHK(hipEventRecord(k.join, k.s2));
       break;
     case OP_BWS:
@@ -648,6 +653,9 @@ static int ensure_sub_streams(Handle* h, int n) {
     Handle::SubStreams& s = h->subs.back();
     HIPCHK(hipStreamCreateWithFlags(&s.s1, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&s.s2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s.s3, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.pfork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.pjoin, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&s.gate, hipEventDisableTiming));
@@ -662,7 +670,8 @@ static int solve_async(Handle* h) {
   const int nsub = sub_batches(h);
   int rc;
   if (nsub <= 1) {
-    const SolveBlock k{h->sp, h->d, h->stream, h->stream2, h->evfork, h->evjoin};
+    const SolveBlock k{h->sp,       h->d,      h->stream,  h->stream2, h->stream3,
+                       h->evfork,   h->evjoin, h->evpfork, h->evpjoin};
     for (const SolveOp& op : ops)
       if ((rc = issue_op(h, k, op))) {
         (void)hipStreamWaitEvent(h->stream, h->evjoin, 0);
@@ -688,6 +697,9 @@ static int solve_async(Handle* h) {
       k.s2 = ss.s2;
       k.fork = ss.fork;
       k.join = ss.join;
+      k.s3 = ss.s3;
+      k.pfork = ss.pfork;
+      k.pjoin = ss.pjoin;
       HIPCHK(hipStreamWaitEvent(k.s1, h->evstart, 0));
     }
     // block s runs `lag` launches behind block s - 1 (its first launch waits on the gate
@@ -1094,13 +1106,17 @@ void api_destroy(Handle* h) {
   if (h->evjoin) (void)hipEventDestroy(h->evjoin);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  if (h->stream3) (void)hipStreamSynchronize(h->stream3);
+  if (h->stream3) (void)hipStreamDestroy(h->stream3);
+  if (h->evpfork) (void)hipEventDestroy(h->evpfork);
+  if (h->evpjoin) (void)hipEventDestroy(h->evpjoin);
   for (Handle::SubStreams& s : h->subs) {
-    for (hipStream_t q : {s.s1, s.s2})
+    for (hipStream_t q : {s.s1, s.s2, s.s3})
       if (q) {
         (void)hipStreamSynchronize(q);
         (void)hipStreamDestroy(q);
       }
-    for (hipEvent_t e : {s.fork, s.join, s.gate, s.done})
+    for (hipEvent_t e : {s.fork, s.join, s.gate, s.done, s.pfork, s.pjoin})
       if (e) (void)hipEventDestroy(e);
   }
   if (h->evstart) (void)hipEventDestroy(h->evstart);
