@@ -210,13 +210,13 @@ def workload_text(name: str) -> str:
 class Solver:
     """One handle on this rank's GPU, stepping init + solve of its batch."""
 
-    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0)):
+    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0, 0)):
         from mhpc_minimal_env_amd import capi
         from mhpc_minimal_env_amd import locomotion as L
         self.capi = capi
         self.loco = L.MHPCLocomotion(desc=desc, option=opt, batch=x0.shape[0], device=device)
         self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2],
-                                     sub_batches=variants[3])
+                                     sub_batches=variants[3], ro_store=variants[4])
         self.loco.set_initial_condition(x0)
         self.lib, self.h = capi.lib(), self.loco._h
         capi.check(self.lib.mhpc_set_x0(self.h, capi.dptr(self.loco._x0)), "mhpc_set_x0")
@@ -320,7 +320,7 @@ def run_sweep(args, torch):
     desc, opt = workload(args.workload)
     for B in [int(b) for b in args.batch_sweep.split(",")]:
         s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant, args.overlap,
-                                                           args.sub_batches))
+                                                           args.sub_batches, args.ro_store))
         for _ in range(args.warmup):
             s.step()
         solve_ms = 0.0
@@ -397,6 +397,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=None,
                     help="steps run after the timed region with per-launch HIP events (kernel "
                          "times, roofline); default = --steps")
+    ap.add_argument("--ro-store", type=int, default=0,
+                    help="line-search trials that store their records (0: default; tuning only)")
     ap.add_argument("--sub-batches", type=int, default=0,
                     help="concurrently scheduled sub-batches per GPU, 1..4 (0 = automatic; tuning only)")
     ap.add_argument("--batch-sweep", default=None,
@@ -447,7 +449,7 @@ def main():
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
     s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant, args.overlap,
-                                                           args.sub_batches))
+                                                           args.sub_batches, args.ro_store))
     for _ in range(args.warmup):
         s.step()
 
