@@ -100,7 +100,7 @@ struct Handle {
   double kms[NKERN] = {}, kbytes[NKERN] = {}, kflops[NKERN] = {};
   int64_t klaunch[NKERN] = {};
   // algorithmic byte model per problem
-  double by_roll_read = 0, by_roll_write = 0, by_par = 0, by_init = 0, by_cost = 0;
+  double by_roll_read = 0, by_roll_write = 0, by_roll_term = 0, by_par = 0, by_init = 0, by_cost = 0;
   // receding horizon (MHPCLocomotion::update_problem): current mode, phase-buffer rotation,
   // buffer store, knot capacity of the packed arrays, and whether the next solve's first
   // forward_sweep(0) must be a real rollout (rotated nominal, new x0)
@@ -156,15 +156,16 @@ constexpr double kB = sizeof(real);  // bytes per element of the solve's arithme
 
 static void byte_model(Handle* h) {
   const SolveParams& sp = h->sp;
-  double rr = 14 * 8, rw = 0, pb = 0, ib = sp.NK * kB, cb = 0;
+  double rr = 14 * 8, rw = 0, rt = 0, pb = 0, ib = sp.NK * kB, cb = 0;
   for (int p = 0; p < sp.P; ++p) {
     const bool wb = p < sp.n_wb;
     const int n = wb ? 14 : 6, N = sp.N[p];
     // nominal x,u (n+4) + K (4n) + du (4) read once per problem (the candidates of a
     // problem share them)
     rr += (N - 1) * kB * ((n + 4) + 4 * n + 4);
-    // each candidate writes x,u,y of every knot (x only at the last knot)
-    rw += (N - 1) * kB * (n + 8) + n * kB;
+    // a storing candidate writes x,u,y of every knot, every candidate x at the last knot
+    rw += (N - 1) * kB * (n + 8);
+    rt += n * kB;
     // k_cost: nominal x,u(,y) of every knot + refpos
     cb += (N - 1) * kB * (n + 4 + (wb ? 4 : 0) + 1) + kB * (n + 1);
     // k_init: x,u,y written for every knot (WB and SRB)
@@ -178,6 +179,7 @@ static void byte_model(Handle* h) {
   }
   h->by_roll_read = rr;
   h->by_roll_write = rw;
+  h->by_roll_term = rt;
   h->by_par = pb;
   h->by_init = ib;
   h->by_cost = cb;
@@ -766,7 +768,13 @@ int api_solve(Handle* h, int32_t* status) {
   if (rc) return rc;
   const unsigned long long* c = h->cnt;
   h->kbytes[K_FULL] += c[C_FWD] * h->by_cost;
-  h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read + c[C_LS_RUN] * h->by_roll_write;
+  {  // the trials that store their records (RO_STORE_FIRST; the re-rolls of the others,
+     // rare, are not counted)
+    const SolveParams& sp = h->sp;
+    const double stored = std::min(sp.n_cand, sp.ro_store + 1);
+    h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read +
+                       c[C_LS_RUN] * (h->by_roll_write * stored / sp.n_cand + h->by_roll_term);
+  }
   h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
   // the SRB half of a split sweep: the SRB knots of every first attempt; the rest (WB knots,
   // impact steps, SRB knots of retries) is the WB half's / the whole sweep's

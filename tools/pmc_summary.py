@@ -24,8 +24,11 @@ def load(path, counter):
             name = r["Kernel_Name"]
             m = re.search(r"mhpc::(\w+)", name)
             key = m.group(1) if m else name
-            if key == "k_bws" and re.search(r"k_bws<\d+, \d+, 1>", name):
-                key = "k_bws_srb"  # SRB half of the split backward sweep
+            if key == "k_bws" and re.search(r"k_bws<\d+, 1, \d+>", name):
+                key = "k_bws_srb"  # SRB half of the split backward sweep (k_bws<RPW, PART 1, RPP>)
+            if key == "k_rollout":  # one launch group: the line search + the re-roll kernel
+                v = re.search(r"k_rollout<(\w+), (\w+), (\w+)>", name)
+                key = "k_rollout." + ("".join(x[0] for x in v.groups()) if v else "x")
             if key == "k_partials":  # one launch group: the two direction groups + impacts
                 g = re.search(r"k_partials<(\d+)>", name)
                 key = f"k_partials.g{g.group(1)}" if g else key
@@ -55,6 +58,16 @@ def main():
             "write_bytes": sum(res[k]["write_bytes"] for k in parts),
             "hbm_bytes_per_launch": sum(res[k]["hbm_bytes_per_launch"] for k in parts),
             "sum_of": parts}
+    # the bench's k_rollout launch = the line-search kernel + the re-roll kernel (mode 2,
+    # k_rollout<false, false, false>, one dispatch per line search)
+    ros = [k for k in res if k.startswith("k_rollout.")]
+    if ros:
+        res["k_rollout"] = {
+            "dispatches": min(res[k]["dispatches"] for k in ros),
+            "fetch_bytes_raw": sum(res[k]["fetch_bytes_raw"] for k in ros),
+            "write_bytes": sum(res[k]["write_bytes"] for k in ros),
+            "hbm_bytes_per_launch": sum(res[k]["hbm_bytes_per_launch"] for k in ros),
+            "sum_of": ros}
     doc = {"source": d, "note": note, "correction": "hbm = 2 * FETCH_SIZE*1024 + WRITE_SIZE*1024",
            "kernels": res}
     with open(out, "w") as fo:
