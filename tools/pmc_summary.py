@@ -22,7 +22,7 @@ def load(path, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            m = re.search(r"mhpc::(\w+)", name)
+            m = re.search(r"mhpc\d*::(\w+)", name)
             key = m.group(1) if m else name
             if key == "k_bws" and re.search(r"k_bws<\d+, 1, \d+>", name):
                 key = "k_bws_srb"  # SRB half of the split backward sweep (k_bws<RPW, PART 1, RPP>)
