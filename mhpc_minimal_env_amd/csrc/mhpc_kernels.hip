@@ -208,7 +208,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
                                                              int max_ddp, int full) {
   MHPC_NO_FMA_F32
   const int nc = full ? 1 : sp.n_cand;
-  const int ppw = PAIR ? min(32 / nc, RO_PAIR_PPB) : 64 / nc;
+  // (a staged re-roll, mode 2: one lane per problem and the stage's ST_PPW problems a block)
+  const int ppw = PAIR ? min(32 / nc, RO_PAIR_PPB) : (ST && full == 2) ? ST_PPW : 64 / nc;
   constexpr int SNP = PAIR ? RO_PAIR_PPB : ST_PPW;  // staged problem slots (ppw <= SNP when staged)
   constexpr bool PF = PAIR && ST && MHPC_RO_PREFETCH;  // register prefetch of the next knot
   const int t = threadIdx.x, lane = t & 63;
@@ -1604,11 +1605,18 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   else
     hipLaunchKernelGGL((k_rollout<false, false, false>), dim3(nblk), dim3(64), 0, s, sp, d,
                        al_iter, ddp_iter, max_ddp, 0);
-  // the accepted trials whose records were not stored (RO_STORE_FIRST), rolled out again
-  // (lane = problem; a block without one returns at once)
-  if (sp.ro_store < sp.n_cand - 1)
-    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
-                       sp, d, al_iter, 0, 0, 2);
+  // the accepted trials whose records were not stored (RO_STORE_FIRST), rolled out again:
+  // lane = problem, ST_PPW problems a block so that their operands go through the LDS stage
+  // (a global round trip per knot otherwise: ~2x the latency); a block without one returns
+  // at once
+  if (sp.ro_store < sp.n_cand - 1) {
+    if (fits)
+      hipLaunchKernelGGL((k_rollout<false, true, false>), dim3((sp.B + ST_PPW - 1) / ST_PPW), dim3(64),
+                         0, s, sp, d, al_iter, 0, 0, 2);
+    else
+      hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
+                         sp, d, al_iter, 0, 0, 2);
+  }
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,

@@ -133,6 +133,8 @@ def test_long_phases_unstaged_line_search(need_gpu):
         assert_oracle(base, O.solve(desc, L.HSDDP_OPTION().to_c(), x0, nthreads=8))
     for ro in ("pair", "fused_staged", "pipe", "fused"):
         assert_bitwise(solve(desc, x0, rollout=ro), base, f"long phases, rollout={ro}")
+    # the unstaged re-roll (an accepted trial without records, one trial stored)
+    assert_bitwise(solve(desc, x0, ro_store=1), base, "long phases, one trial stored")
 
 
 @pytest.mark.parametrize("name,precision", [("c3", 64), ("c5", 64), ("c5", 32)])
