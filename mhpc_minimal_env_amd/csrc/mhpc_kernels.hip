@@ -1017,9 +1017,9 @@ hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, in
 // system at the knot's solution (mhpc_model.h, WbKnot): the lane solves the knot's forward
 // dynamics once and then, per tangent direction, evaluates the inverse-dynamics residual in
 // dual numbers and solves with the knot's own factorisation.  Two launches over the knot
-// grid, a lane per (problem, WB knot) each: G = 0 the configuration directions 2..6, G = 1
-// the velocity directions 9..13 and the controls 14..17 plus the knot's control / force cost
-// derivatives; directions 0, 1, 7, 8 (base position / velocity) are exact zeros written
+// grid, a lane per (problem, WB knot) each: G = 0 the configuration directions 2..6 (plus
+// the knot's control / force cost derivatives), G = 1 the velocity directions 9..13 and the
+// controls 14..17; directions 0, 1, 7, 8 (base position / velocity) are exact zeros written
 // once at create.  k_partials_impact: the impact Jacobian Px at the end of the touchdown
 // phases, one lane per (problem, impact, direction), dual numbers through wb_impact.
 // ============================================================================================
@@ -1087,8 +1087,7 @@ __global__ __launch_bounds__(256, MHPC_PAR_MINB) void k_partials(SolveParams sp,
   if (mode == 1) partials_knot<kBack, G>(nk, rec);
   else if (mode == 3) partials_knot<kFront, G>(nk, rec);
   else partials_knot<-1, G>(nk, rec);
-  if (G == kParGroups - 1) {  // (with the lighter velocity / control group: the groups
-    // run side by side on two streams and finish together)
+  if (G == 0) {
     // running-cost derivatives of controls and contact forces at the nominal knot
     // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
     real c[14];
