@@ -4,8 +4,10 @@
     before it was skipped -- the checker must flag that shape and pass the legal placements;
   * DPP read-after-write hazards (round 4): the sweep's row-broadcast multiply-adds are inline
     assembly (mhpc_dpp.h), outside the compiler's hazard recognizer; a DPP instruction may not
-    read a VGPR written in the previous 2 wait states.
-Both must pass every kernel TU of the shipping build."""
+    read a VGPR written in the previous 2 wait states;
+  * no scratch memory in the solve's kernels (round 4): a scratch access waits on gfx950's
+    single in-order VM counter behind every earlier global store.
+All must pass every kernel TU of the shipping build."""
 import os
 import subprocess
 import sys
@@ -16,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import check_exec_prologue as C  # noqa: E402
 import check_dpp_hazards as D  # noqa: E402
+import check_no_scratch as S  # noqa: E402
 
 CSRC = os.path.join(ROOT, "mhpc_minimal_env_amd", "csrc")
 
@@ -58,6 +61,25 @@ def test_dpp_hazard_checker(tmp_path):
     assert sorted(b.split(": ")[1] for b in bad) == ["acc_hazard", "label_hazard", "src_hazard"]
 
 
+def test_no_scratch_checker(tmp_path):
+    """A hot kernel with a scratch instruction or a private segment is flagged; the debug-info
+    kernel (not in the solve) and kernels outside the solve are not."""
+    def kern(name, body, priv):
+        return (f"{name}:\n{body}\n.Lfunc_end{name}:\n", f"  - .name: {name}\n"
+                f"    .private_segment_fixed_size: {priv}\n")
+    parts = [kern("_ZN4mhpc9k_rolloutILb1EEEv", "\tscratch_store_dwordx2 v0, v[2:3], off", 0),
+             kern("_ZN4mhpc5k_bwsILi2EEEv", "\tv_mov_b32_e32 v0, 0", 16),
+             kern("_ZN4mhpc6k_initEv", "\tv_mov_b32_e32 v0, 0", 0),
+             kern("_ZN4mhpc11k_cost_gradEv", "\tscratch_load_dword v0, off, s0", 8),
+             kern("_ZN4mhpc8k_exportEv", "\tscratch_load_dword v0, off, s0", 8)]
+    p = tmp_path / "k.s"
+    p.write_text("".join(a for a, _ in parts) + "amdhsa.kernels:\n" + "".join(b for _, b in parts))
+    bad = S.check(str(p))
+    assert len(bad) == 2
+    assert any("k_rollout" in b and "1 scratch instructions" in b for b in bad)
+    assert any("k_bws" in b and "private segment 16" in b for b in bad)
+
+
 def test_generated_dpp_header_is_current():
     """mhpc_dpp.h is what tools/gen_dpp_asm.py generates."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_dpp_asm.py")],
@@ -74,6 +96,7 @@ def test_shipping_kernels_have_no_misplaced_join_copy():
     assert C.scan_all(isa) == []
     sweeps = [os.path.join(CSRC, "_build", f) for f in ("bws.s", "bws32.s")]
     assert D.main(sweeps) == 0
+    assert S.main(isa) == 0
     for p in sweeps:  # the row-broadcast FMAs are there (the gate checked something)
         with open(p) as f:
             assert f.read().count("_dpp ") > 1000
