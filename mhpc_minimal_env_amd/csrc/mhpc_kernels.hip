@@ -1636,7 +1636,8 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real
 // The direction groups write disjoint columns of the records: with a second stream s3 the
 // velocity / control group (G = 1, 252 VGPRs, two waves per SIMD) runs beside the
 // configuration group (340 VGPRs, one wave per SIMD) and fills the SIMDs its tail leaves;
-// s joins s3 before returning.
+// the impact Jacobians (px: they read only the nominal) follow the shorter group on s3; s
+// joins s3 before returning.
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s, hipStream_t s3,
                            hipEvent_t fork, hipEvent_t join) {
   const long tk = (long)sp.B * sp.par_knots, ti = (long)sp.B * sp.par_imp;
@@ -1656,7 +1657,8 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
     }
   }
   if (ti > 0)
-    hipLaunchKernelGGL(k_partials_impact, dim3((unsigned)((ti + 255) / 256)), dim3(256), 0, s, sp, d);
+    hipLaunchKernelGGL(k_partials_impact, dim3((unsigned)((ti + 255) / 256)), dim3(256), 0, two ? s3 : s,
+                       sp, d);
   if (two) {
     hipError_t e = hipEventRecord(join, s3);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
