@@ -1103,7 +1103,13 @@ int api_reset_kernel_stats(Handle* h) {
 void api_destroy(Handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  // every stream of the handle drains before its buffers go (an error inside a solve can
+  // leave work queued on the partials' or a sub-batch's streams)
+  for (hipStream_t q : {h->stream, h->stream2, h->stream3})
+    if (q) (void)hipStreamSynchronize(q);
+  for (Handle::SubStreams& s : h->subs)
+    for (hipStream_t q : {s.s1, s.s2, s.s3})
+      if (q) (void)hipStreamSynchronize(q);
   free_bufs(h);
   if (h->dcnt) (void)hipFree(h->dcnt);
   if (h->store) (void)hipFree(h->store);
@@ -1112,18 +1118,13 @@ void api_destroy(Handle* h) {
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->evfork) (void)hipEventDestroy(h->evfork);
   if (h->evjoin) (void)hipEventDestroy(h->evjoin);
-  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
-  if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->evpfork) (void)hipEventDestroy(h->evpfork);
   if (h->evpjoin) (void)hipEventDestroy(h->evpjoin);
   for (Handle::SubStreams& s : h->subs) {
     for (hipStream_t q : {s.s1, s.s2, s.s3})
-      if (q) {
-        (void)hipStreamSynchronize(q);
-        (void)hipStreamDestroy(q);
-      }
+      if (q) (void)hipStreamDestroy(q);
     for (hipEvent_t e : {s.fork, s.join, s.gate, s.done, s.pfork, s.pjoin})
       if (e) (void)hipEventDestroy(e);
   }
