@@ -125,6 +125,39 @@ def cpu_baseline(desc, opt, sample: int, threads: int, label: str = "C3"):
     }, None
 
 
+def cpu_baseline_mixed(args, opt, threads: int):
+    """The CPU oracle on a sample of the mixed workload: the first `n` problems of the same
+    global stream (layout b % 6), solved layout by layout on `threads` threads; value = problems
+    / total wall time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle as O
+    except Exception as e:  # pragma: no cover
+        return None, f"oracle import failed: {e}"
+    if not O.available():
+        return None, "oracle/_ref not built on this machine"
+    descs, _ = layouts_of("mixed", 6)
+    # about 15 s of CPU work: C5 problems cost ~3x a C3 problem
+    n = args.cpu_sample or 6 * max(1, int(cpu_sample_for(descs[0], opt, threads, seconds=15.0) / 10))
+    lay = layouts_of("mixed", n)[1]
+    x0 = x0_of("mixed", descs[0], n)
+    dt = 0.0
+    for l, d in enumerate(descs):
+        idx = np.where(lay == l)[0]
+        if len(idx) == 0:
+            continue
+        xl = x0[idx] if d.n_wb > 0 else x0[idx][:, :6]
+        t0 = time.perf_counter()
+        O.solve(d, opt.to_c(), xl, nthreads=threads)
+        dt += time.perf_counter() - t0
+    return {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
+            "sample": (f"{n} mixed-workload problems (same x0 stream and layouts), init+solve "
+                       f"{dt:.2f} s wall, the CPU restatement of MultiPhaseDDP::solve calling the "
+                       f"reference's CasADi kernels (oracle/_ref), one problem per thread on "
+                       f"{threads} threads, layout by layout")}, None
+
+
 def cpu_sample_for(desc, opt, threads: int, seconds: float) -> int:
     """Problems for about `seconds` of CPU-baseline work: time a probe of 2 problems per
     thread and scale (the GPU box's host speed is not known in advance)."""
@@ -193,28 +226,57 @@ def roofline_of(stats: dict, batch: int, wl: str = "c3") -> dict:
 def workload(name: str):
     from mhpc_minimal_env_amd import configs
     from mhpc_minimal_env_amd import locomotion as L
+    if name == "mixed":
+        return configs.mixed_descs()[0], L.HSDDP_OPTION()
     return getattr(configs, f"{name}_desc")(), L.HSDDP_OPTION()
 
 
+def layouts_of(name: str, B: int, offset: int = 0):
+    """Per-problem layouts of a workload: (descs, layout of each problem) or None.  mixed:
+    global problem g takes configs.mixed_descs()[g % 6] (C3 at its four gait points, C5 at two)."""
+    if name != "mixed":
+        return None
+    from mhpc_minimal_env_amd import configs
+    descs = configs.mixed_descs()
+    return descs, ((offset + np.arange(B)) % len(descs)).astype(np.int32)
+
+
+def x0_of(name: str, desc, B: int, offset: int = 0):
+    from mhpc_minimal_env_amd import configs
+    lay = layouts_of(name, B, offset)
+    if lay is None:
+        return configs.x0_for(desc, B, offset=offset)
+    return configs.x0_rows(lay[0], lay[1], offset=offset)
+
+
 def metric_of(name: str) -> str:
+    if name == "mixed":
+        return "MHPC solves/sec (mixed gait schedules: 2WB+2SRB trot at 4 gait points, 4WB+6SRB bound at 2)"
     return ("MHPC solves/sec (2WB+2SRB trot)" if name == "c3"
             else "MHPC solves/sec (4WB+6SRB bound)" + (", fp32" if name == "c5f32" else ""))
 
 
 def workload_text(name: str) -> str:
-    return (("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, N=80/phase"
-             if name == "c3" else "C5: Gait() BOUND, 4 WB + 6 SRB, N=80/100 alternating")
-            + ", HSDDP max_AL=2 max_DDP=3; step = initialization + solve of the whole batch")
+    if name == "mixed":
+        head = ("mixed: problem b has its own phase layout, configs.mixed_descs()[b % 6] = C3 "
+                "(2 WB + 2 SRB, PRONK 0.08 s) starting at mode 1 / 2 / 3 / 4 and C5 (4 WB + 6 SRB, "
+                "BOUND) starting at mode 1 / 3, one handle, every launch over all six layouts")
+    else:
+        head = ("C3: 2 WB (modes 1,2) + 2 SRB (modes 3,4), Gait(PRONK) 0.08 s, N=80/phase"
+                if name == "c3" else "C5: Gait() BOUND, 4 WB + 6 SRB, N=80/100 alternating")
+    return head + ", HSDDP max_AL=2 max_DDP=3; step = initialization + solve of the whole batch"
 
 
 class Solver:
     """One handle on this rank's GPU, stepping init + solve of its batch."""
 
-    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0, 0)):
+    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0, 0), layouts=None):
         from mhpc_minimal_env_amd import capi
         from mhpc_minimal_env_amd import locomotion as L
         self.capi = capi
         self.loco = L.MHPCLocomotion(desc=desc, option=opt, batch=x0.shape[0], device=device)
+        if layouts is not None:  # per-problem phase layouts (gait schedules)
+            self.loco.set_layouts(*layouts)
         self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2],
                                      sub_batches=variants[3], ro_store=variants[4])
         self.loco.set_initial_condition(x0)
@@ -319,8 +381,9 @@ def run_sweep(args, torch):
     from mhpc_minimal_env_amd import configs
     desc, opt = workload(args.workload)
     for B in [int(b) for b in args.batch_sweep.split(",")]:
-        s = Solver(desc, opt, configs.x0_for(desc, B), 0, (args.bws_variant, args.ro_variant, args.overlap,
-                                                           args.sub_batches, args.ro_store))
+        s = Solver(desc, opt, x0_of(args.workload, desc, B), 0,
+                   (args.bws_variant, args.ro_variant, args.overlap, args.sub_batches, args.ro_store),
+                   layouts=layouts_of(args.workload, B))
         for _ in range(args.warmup):
             s.step()
         solve_ms = 0.0
@@ -368,10 +431,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="problems per GPU (default: c3 1024, c5 4096, c2 1)")
-    ap.add_argument("--workload", choices=["c3", "c5", "c5f32", "c2"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c5", "c5f32", "c2", "mixed"], default="c3",
                     help="c3: the headline 2WB+2SRB solve (BASELINE configs[2]); c5: 4WB+6SRB "
                          "bound solve (fp64), c5f32: the same in the fp32 instantiation "
-                         "(BASELINE configs[4]); c2: 256 trial rollouts of one nominal per problem")
+                         "(BASELINE configs[4]); c2: 256 trial rollouts of one nominal per problem; "
+                         "mixed: per-problem gait schedules (C3 / C5 layouts at several gait "
+                         "points in one batch)")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="c3 at N=1: skip the extra batch-4096 measurement (north_star_b4096)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="CPU-baseline problems (default: ~15 s of CPU work on the usable cores)")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -443,13 +510,14 @@ def main():
 
     from mhpc_minimal_env_amd import configs, sharding
 
-    B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c5f32": 4096, "c2": 1}[args.workload]
+    B = args.batch_per_gpu or {"c3": 1024, "c5": 4096, "c5f32": 4096, "c2": 1,
+                               "mixed": 4096}[args.workload]
     desc, opt = workload(args.workload)
-    x0 = configs.x0_for(desc, B, offset=rank * B)
+    x0 = x0_of(args.workload, desc, B, offset=rank * B)
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
-    s = Solver(desc, opt, x0, local_rank, (args.bws_variant, args.ro_variant, args.overlap,
-                                                           args.sub_batches, args.ro_store))
+    variants = (args.bws_variant, args.ro_variant, args.overlap, args.sub_batches, args.ro_store)
+    s = Solver(desc, opt, x0, local_rank, variants, layouts=layouts_of(args.workload, B, rank * B))
     for _ in range(args.warmup):
         s.step()
 
@@ -501,7 +569,8 @@ def main():
         if shard is not None and not args.no_shard_check:
             # the same global x0 stream solved on one GPU: every gathered summary must be
             # bitwise identical
-            one = Solver(desc, opt, configs.x0_for(desc, world * B), local_rank)
+            one = Solver(desc, opt, x0_of(args.workload, desc, world * B), local_rank,
+                         layouts=layouts_of(args.workload, world * B))
             one.step()
             ref = one.summary(0)
             one.close()
@@ -511,11 +580,34 @@ def main():
             if not same:
                 print("bench.py: sharded results differ from the 1-GPU solve", file=sys.stderr)
         total = world * B * args.steps
+        # north star (BASELINE.json: solves/s at batch 4096 on one GPU): the same init + solve
+        # step at 4096 problems, measured in this run after the headline's timed region
+        ns = None
+        if (world == 1 and args.workload == "c3" and B != 4096 and not args.no_north_star
+                and dist is None):
+            n4 = 4096
+            s4 = Solver(desc, opt, x0_of("c3", desc, n4), local_rank)
+            for _ in range(args.warmup):
+                s4.step()
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            for _ in range(args.steps):
+                s4.step()
+            torch.cuda.synchronize()
+            d4 = time.perf_counter() - t4
+            s4.close()
+            ns = {"batch": n4, "value": n4 * args.steps / d4, "unit": "solves/s",
+                  "ms_per_step": d4 / args.steps * 1e3, "steps": args.steps,
+                  "note": "same step (initialization + solve of the whole batch) at the north-star "
+                          "batch, timed after the headline's timed region"}
         cpu, why = (None, "disabled" if world == 1 else "reported at N=1 only")
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or usable_cpus()
-            sample = args.cpu_sample or cpu_sample_for(desc, opt, threads, seconds=15.0)
-            cpu, why = cpu_baseline(desc, opt, sample, threads, label=args.workload.upper()[:2])
+            if args.workload == "mixed":
+                cpu, why = cpu_baseline_mixed(args, opt, threads)
+            else:
+                sample = args.cpu_sample or cpu_sample_for(desc, opt, threads, seconds=15.0)
+                cpu, why = cpu_baseline(desc, opt, sample, threads, label=args.workload.upper()[:2])
         line = {
             "metric": metric_of(args.workload),
             "value": total / dt,
@@ -531,6 +623,7 @@ def main():
             "data": "synthetic (x0 = reference default + splitmix64 perturbation)",
             "config": {
                 "workload": workload_text(args.workload),
+                **({"layouts": len(layouts_of("mixed", 6)[0])} if args.workload == "mixed" else {}),
                 "batch_per_gpu": B,
                 "global_batch": world * B,
                 "parallelism": f"batch-sharded x{world}",
@@ -542,6 +635,8 @@ def main():
             "roofline": roofline_of(stats, B, args.workload),
             "cpu_baseline": cpu if cpu is not None else {"value": None, "reason": why},
         }
+        if ns is not None:
+            line["north_star_b4096"] = ns
         if shard is not None:
             line["sharding"] = shard
         print(json.dumps(line), file=_LINE_OUT or sys.stdout, flush=True)

@@ -39,6 +39,7 @@ extern "C" {
 
 #define MHPC_MAX_PHASES 16
 #define MHPC_MAX_KNOTS 1024
+#define MHPC_MAX_LAYOUTS 32   /* distinct phase layouts (gait schedules) per handle */
 #define MHPC_TRACE_LEN 64
 
 typedef enum {
@@ -152,8 +153,41 @@ typedef struct {
  * parameters.  Then call mhpc_solve again.  The phase descriptor reported by
  * mhpc_get_desc changes accordingly. */
 int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait);
-/* The handle's current phase layout (changes with mhpc_update_problem). */
+/* The handle's current phase layout (changes with mhpc_update_problem); with per-problem
+ * layouts (mhpc_set_layouts) the layout of problem 0. */
 int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc);
+
+/* ---- per-problem phase layouts: the batch axis over gait schedules --------------------
+ * In the reference every controller instance builds its phase layout from its own Gait and
+ * gait point (MHPCLocomotion::build_problem, MHPCLocomotion.cpp:63-104; Gait.h:21-77) and
+ * rotates it per control tick (update_problem, :107-158).  A handle starts with the
+ * descriptor of mhpc_create for every problem; mhpc_set_layouts gives problem b the
+ * descriptor descs[layout_of_problem[b]] (1 <= n_desc <= MHPC_MAX_LAYOUTS; precision,
+ * vel_cmd and height_cmd must equal the handle's; NULL layout_of_problem: descs[b % n_desc]).
+ * The arrays grow when a layout has more knots than any before.  The handle is then
+ * uninitialised: mhpc_set_x0 (rows of 14 when any layout has a whole-body phase -- an
+ * SRB-only problem reads the first 6 of its row -- else 6) and mhpc_initialize precede the
+ * next solve.  Problems sharing a layout are solved together, a launch never mixes layouts
+ * inside a block, and each problem's arithmetic is the one it gets in a handle of its own
+ * layout, bit for bit (tests/test_gpu_layouts.py).  Outputs: mhpc_get_phase_problems needs
+ * a problem range whose phase has one shape (knots, state size); mhpc_get_scalars' V_phase /
+ * dV_phase rows are max-phase-count long, zero past a problem's phases. */
+int mhpc_set_layouts(mhpc_handle* h, int n_desc, const mhpc_problem_desc* descs,
+                     const int32_t* layout_of_problem);
+/* The current phase layout of problem b (changes with mhpc_update_problem[s]). */
+int mhpc_get_problem_desc(mhpc_handle* h, int problem, mhpc_problem_desc* desc);
+/* Per-problem MHPCLocomotion::update_problem: problem b takes steps[b] >= 0 gait steps of
+ * gaits[gait_of_problem[b]] (one step = one update_problem: the WB / SRB phase buffers
+ * rotate by one, the next mode starts the horizon, knot counts round(timing / dt)); with
+ * steps[b] = 0 it keeps its layout and warm start.  Every problem's references are then
+ * regenerated from its current x0 and its AL / ReB parameters re-initialised, as
+ * update_problem does, and the next mhpc_solve starts from the (rotated) solutions.
+ * NULL gait_of_problem: gaits[0] for every problem; NULL steps: one step each (then this is
+ * mhpc_update_problem).  n_gaits in 1..MHPC_MAX_LAYOUTS. */
+int mhpc_update_problems(mhpc_handle* h, int n_gaits, const mhpc_gait* gaits,
+                         const int32_t* gait_of_problem, const int32_t* steps);
+/* Distinct phase layouts currently in use (1 for a homogeneous batch). */
+int mhpc_num_layouts(mhpc_handle* h, int* n);
 
 /* ---- cost and constraint parameters (the reference's downward plugin points) --------
  * The reference's solve reads its weights through CostAbstract / Cost<T,X,U,Y>
@@ -206,6 +240,10 @@ int mhpc_get_constraint_params(mhpc_handle* h, mhpc_constraint_params* c);
  * (MHPCLocomotion.cpp:355-377; AL terms in Phix only after forward_sweep(0), quirk B1).
  * Either pointer may be NULL. */
 int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, double* Phix);
+/* The same for problems [first, first + count) (rows of count in place of batch); with
+ * per-problem layouts the range's phase must have one shape. */
+int mhpc_get_cost_gradients_problems(mhpc_handle* h, int phase, int first, int count, double* lx,
+                                     double* Phix);
 
 /* The trial rollouts of MultiPhaseDDP::forward_iteration (MultiPhaseDDP.cpp:130-151, i.e.
  * SinglePhase::forward_sweep_dynamics_only, SinglePhase.cpp:117-144, chained over phases by

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("MHPC_AMD_LIB") or os.path.join(HERE, "libmhpc_amd.so"
 
 MHPC_MAX_PHASES = 16
 MHPC_MAX_KNOTS = 1024
+MHPC_MAX_LAYOUTS = 32
 MHPC_TRACE_LEN = 64
 MHPC_NUM_KERNELS = 7
 MHPC_MAX_ROLLOUT_EPS = 4096
@@ -188,8 +189,17 @@ SIGNATURES = [
     ("mhpc_get_scalars", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, _DP, _IP]),
     ("mhpc_get_counters", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Counters)]),
     ("mhpc_get_cost_gradients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP]),
+    ("mhpc_get_cost_gradients_problems", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                        ctypes.c_int, _DP, _DP]),
     ("mhpc_update_problem", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GaitC)]),
+    ("mhpc_update_problems", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(GaitC),
+                                            _IP, _IP]),
     ("mhpc_get_desc", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ProblemDesc)]),
+    ("mhpc_set_layouts", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ProblemDesc),
+                                        _IP]),
+    ("mhpc_get_problem_desc", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.POINTER(ProblemDesc)]),
+    ("mhpc_num_layouts", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     ("mhpc_rollout_costs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP,
                                           ctypes.POINTER(ctypes.c_float)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),

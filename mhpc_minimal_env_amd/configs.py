@@ -48,6 +48,40 @@ def demo_desc():
     return L.desc_from_params(L.MHPCUserParameters(usrcmd=L.USRCMD(vel=1.5)), L.Gait())
 
 
+def c3_at(cmode: int):
+    """C3 at another point of its gait cycle: the layout MHPCLocomotion::build_problem makes
+    for a controller whose current mode is cmode (the PRONK / default-branch gait)."""
+    params = L.MHPCUserParameters(n_wbphase=2, n_fbphase=2, cmode=cmode, usrcmd=L.USRCMD(vel=1.5))
+    return L.desc_from_params(params, L.Gait(L.GaitType2D.PRONK))
+
+
+def c5_at(cmode: int, precision: int = 64):
+    """C5 (bound) at current mode cmode."""
+    params = L.MHPCUserParameters(n_wbphase=4, n_fbphase=6, cmode=cmode, usrcmd=L.USRCMD(vel=1.5))
+    d = L.desc_from_params(params, L.Gait())
+    d.precision = precision
+    return d
+
+
+def mixed_descs():
+    """The mixed workload (north_star's batch axis over gait schedules): controllers at every
+    point of the C3 trot cycle and at two points of the C5 bound cycle; problem b takes
+    layout b % 6 (two thirds C3, one third C5)."""
+    return [c3_at(1), c3_at(2), c3_at(3), c3_at(4), c5_at(1), c5_at(3)]
+
+
+def x0_rows(descs, layout_of_problem, offset: int = 0):
+    """Initial states of a mixed batch (rows of 14; an SRB-only problem's state in the first
+    6 entries of its row, as mhpc_set_x0 reads it), the same stream as x0_for."""
+    lop = np.asarray(layout_of_problem)
+    x0 = L.random_x0(len(lop), offset=offset)
+    for b, l in enumerate(lop):
+        if descs[l].n_wb == 0:
+            x0[b, :6] = x0[b, L.STATE_PROJ_ROWS]
+            x0[b, 6:] = 0
+    return np.ascontiguousarray(x0)
+
+
 def x0_for(desc, batch: int, offset: int = 0):
     x0 = L.random_x0(batch, offset=offset)
     if desc.n_wb == 0:

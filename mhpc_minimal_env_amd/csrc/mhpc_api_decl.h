@@ -15,8 +15,13 @@ int api_batch(Handle* h);
 int api_get_scalars(Handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
                     double* dV_phase, int32_t* trace);
 int api_rollout_costs(Handle* h, int n_eps, const double* eps, double* J, double* viol, float* ms);
-int api_get_cost_gradients(Handle* h, int phase, double* lx, double* Phix);
+int api_get_cost_gradients(Handle* h, int phase, int first, int count, double* lx, double* Phix);
 int api_update_problem(Handle* h, const mhpc_gait* gait);
+int api_update_problems(Handle* h, int n_gaits, const mhpc_gait* gaits, const int32_t* gait_of,
+                        const int32_t* steps);
+int api_set_layouts(Handle* h, int n_desc, const mhpc_problem_desc* descs, const int32_t* lop);
+int api_get_problem_desc(Handle* h, int b, mhpc_problem_desc* desc);
+int api_num_layouts(Handle* h, int* n);
 int api_get_desc(Handle* h, mhpc_problem_desc* desc);
 int api_get_counters(Handle* h, mhpc_counters* c);
 int api_set_profiling(Handle* h, int on);

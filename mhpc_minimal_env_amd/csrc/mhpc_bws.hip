@@ -254,13 +254,13 @@ __device__ __forceinline__ bool any_go(const RowCtx& r) {
 // then lu, luu, ly, lyy) is read straight into the lanes that own its columns; the next
 // knot's record is loaded while the current one computes.
 template <bool STANCE>
-__device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+__device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                          RowCtx& rc, int p) {
   using R = Rows<7>;
   using wk = wreal;
   const int t = rc.t, b = rc.b;
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const real dt = sp.dt[p];
+  const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
+  const real dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 14;
   const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
@@ -515,13 +515,13 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const ProbStat
 // entry is computed with the one-row sweep's operations in the same order, so the two
 // layouts agree bit for bit (tests/test_gpu_variants.py).
 template <bool STANCE>
-__device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+__device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<7>;
   using wk = wreal;
   const int t = rc.t, b = rc.b, rp = rc.rp;
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const real dt = sp.dt[p];
+  const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
+  const real dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 14;
   const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
@@ -774,12 +774,12 @@ __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const
 // ---------------------------------------------------------------------------------------
 // SRB phase (NQ = 3): the Jacobians are evaluated in registers (FBDynamics_par.c), the cost
 // derivatives from the nominal knot (CostBase.cpp:19-34).
-__device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbState* st, RowLds& rl,
+__device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<3>;
   const int t = rc.t, b = rc.b;
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
-  const real dt = sp.dt[p];
+  const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
+  const real dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 6;
   const int cj = rho < 10 ? rho : 0;  // column of [A B] held (clamped for spare lanes)
@@ -947,10 +947,10 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const ProbSta
 // H = Phixx + Hnext; AL partials only while st->al_partials (quirk B1).  G of knot N-1 is
 // an output of the phase.
 template <int NX>
-__device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const ProbState* st,
+__device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st,
                                RowLds& rl, const RowCtx& rc, int p) {
   constexpr bool wb = NX == 14;
-  const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+  const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
   const real pos = d.refpos[(size_t)rc.b * sp.NK + ko + N - 1];
   const real* xe = traj_ptr(sp, d, rc.b, rc.nom, ko + N - 1);
   const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
@@ -999,11 +999,11 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const Pr
 
 // impact_aware_step (MultiPhaseDDP.cpp:300-341) for a WB phase p: rl.M / rl.Gs hold CTG[0] of
 // phase p+1 (6-dim if that phase is SRB); on exit the 14-dim Gnext / Hnext of phase p.
-__device__ void impact_step(const SolveParams& sp, const DevBufs& d, RowLds& rl, RowCtx& rc, int p) {
+__device__ void impact_step(const SolveParams& sp, const DevBufs& d, const Layout& L, RowLds& rl, RowCtx& rc, int p) {
   using R = Rows<7>;
   const int t = rc.t;
-  const int mode = sp.mode[p];
-  const bool nwb = p + 1 < sp.n_wb;
+  const int mode = L.mode[p];
+  const bool nwb = p + 1 < L.n_wb;
   const bool imp = mode == 2 || mode == 4;
   const int i = t < 14 ? R::rho(t) : 0;
   // lift to the full-model space: E' G', E' H' E (E = _stateProj for an SRB next phase)
@@ -1079,15 +1079,15 @@ __device__ unsigned long long g_bws_cyc[8];
 // kernel (its register allocation is the SRB knot's, so a partials wave fits beside it).
 // RPP: rows per problem (2: the whole-body phases run sweep_wb2, SRB phases on both rows).
 template <bool WB_CODE, int RPP>
-__device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState* st, RowLds& rl,
+__device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layout& L, ProbState* st, RowLds& rl,
                              RowCtx& rc, int p_hi, int p_lo) {
   for (int p = p_hi; p >= p_lo; --p) {
-    const bool wb = WB_CODE && p < sp.n_wb;
+    const bool wb = WB_CODE && p < L.n_wb;
     const bool was_go = go(rc);
-    if (p + 1 < sp.P) {
+    if (p + 1 < L.P) {
       if constexpr (WB_CODE) {
         BWS_T(ti0);
-        if (wb) impact_step(sp, d, rl, rc, p);
+        if (wb) impact_step(sp, d, L, rl, rc, p);
         BWS_ADD(5, clock64() - ti0);
       }
       if (was_go) rc.dV = st->dV[p + 1];  // dVnext
@@ -1095,27 +1095,27 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, ProbState*
     BWS_T(tt0);
     if (wb) {
       if constexpr (WB_CODE) {
-        terminal_value<14>(sp, d, st, rl, rc, p);
+        terminal_value<14>(sp, d, L, st, rl, rc, p);
         BWS_ADD(4, clock64() - tt0);
         BWS_T(tw0);
-        const int mode = sp.mode[p];
+        const int mode = L.mode[p];
         if (RPP == 2) {
-          if (mode == 1 || mode == 3) sweep_wb2<true>(sp, d, st, rl, rc, p);
-          else sweep_wb2<false>(sp, d, st, rl, rc, p);
+          if (mode == 1 || mode == 3) sweep_wb2<true>(sp, d, L, st, rl, rc, p);
+          else sweep_wb2<false>(sp, d, L, st, rl, rc, p);
         } else {
-          if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, st, rl, rc, p);
-          else sweep_wb<false>(sp, d, st, rl, rc, p);
+          if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, L, st, rl, rc, p);
+          else sweep_wb<false>(sp, d, L, st, rl, rc, p);
         }
         BWS_ADD(0, clock64() - tw0);
-        BWS_ADD(1, sp.N[p] - 1);
+        BWS_ADD(1, L.N[p] - 1);
       }
     } else {
-      terminal_value<6>(sp, d, st, rl, rc, p);
+      terminal_value<6>(sp, d, L, st, rl, rc, p);
       BWS_ADD(4, clock64() - tt0);
       BWS_T(ts0);
-      sweep_srb(sp, d, st, rl, rc, p);
+      sweep_srb(sp, d, L, st, rl, rc, p);
       BWS_ADD(2, clock64() - ts0);
-      BWS_ADD(3, sp.N[p] - 1);
+      BWS_ADD(3, L.N[p] - 1);
     }
     if (was_go && rc.lt == 0) st->dV[p] = rc.dV;
     if (!any_go(rc)) break;
@@ -1160,10 +1160,14 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
   rc.rp = RPP == 2 ? row & 1 : 0;
   rc.lt = rc.t + 16 * rc.rp;
   rc.nl = 16 * RPP;
-  const int b0 = blockIdx.x * RPW + q;
-  rc.b = b0 < sp.B ? b0 : sp.B - 1;
+  // the block's layout group and problems (a block never mixes layouts)
+  const GrpBlk gb = block_group(sp, blockIdx.x, RPW);
+  if (gb.g < 0) return;
+  const Layout& L = layout_of(d, gb.g);
+  const bool inb = q < RPW && gb.p0 + q < gb.p1;
+  rc.b = prob_at(sp, d, inb ? gb.p0 + q : gb.p0);  // a spare row shadows the block's first problem
   ProbState* st = &d.st[rc.b];
-  rc.act = q < RPW && b0 < sp.B && st->active && st->ddp_active;
+  rc.act = inb && st->active && st->ddp_active;
   if (!__builtin_amdgcn_ballot_w64(rc.act)) return;
   RowLds& rl = sh.r[q];
   rc.nom = st->nom_slot;
@@ -1180,7 +1184,8 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     sweeps += rc.live ? 1 : 0;
     if (PART == 1) {
       zero_value(rl, rc);
-      sweep_phases<false, 1>(sp, d, st, rl, rc, sp.P - 1, sp.n_wb);
+      // (a layout without SRB phases passes with nothing swept; PART 2 sweeps it whole)
+      if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
       BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       if (rc.act) {
@@ -1194,7 +1199,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       }
       return;
     }
-    if (PART == 2 && first) {
+    if (PART == 2 && first && L.P > L.n_wb) {
       // resume from the SRB half's value function (or retry if that half failed)
       const BwsCarry& c = d.carry[rc.b];
       __syncthreads();
@@ -1204,11 +1209,11 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       __syncthreads();
       rc.failed = rc.live && c.ok == 0;
       rc.kn += rc.live ? c.knots : 0;
-      rc.dV = st->dV[sp.n_wb];
-      sweep_phases<true, RPP>(sp, d, st, rl, rc, sp.n_wb - 1, 0);
+      rc.dV = st->dV[L.n_wb];
+      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
-      sweep_phases<true, RPP>(sp, d, st, rl, rc, sp.P - 1, 0);
+      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, 0);
     }
     pending = rc.live && rc.failed;
     if (pending) {
@@ -1257,17 +1262,24 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
 #ifndef MHPC_BWS_PAIRS_MAX_B
 #define MHPC_BWS_PAIRS_MAX_B 2048
 #endif
+int launch_problems(const SolveParams& sp);
+// Blocks of `rpw` problems over the layout groups (block_group)
+static unsigned bws_grid(const SolveParams& sp, int rpw) {
+  long n = 0;
+  for (int g = 0; g < sp.ngrp; ++g) n += (sp.go[g + 1] - sp.go[g] + rpw - 1) / rpw;
+  return (unsigned)n;
+}
 int bws_auto_variant(int B) {
   return B <= MHPC_BWS_PAIRS_MAX_B ? MHPC_VARIANT_BWS_PAIRS2 : MHPC_VARIANT_BWS_ROWS4;
 }
 
 hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, int part,
                       hipStream_t s) {
-  const int v = sp.var_bws ? sp.var_bws : bws_auto_variant(sp.B);
+  const int v = sp.var_bws ? sp.var_bws : bws_auto_variant(launch_problems(sp));
   const int rpw = v == MHPC_VARIANT_BWS_ROWS1 ? 1 : (v == MHPC_VARIANT_BWS_ROWS2 ||
                                                      v == MHPC_VARIANT_BWS_PAIRS2) ? 2 : 4;
-  const dim3 grid((sp.B + rpw - 1) / rpw);
-  const dim3 grid4((sp.B + 3) / 4);
+  const dim3 grid(bws_grid(sp, rpw));
+  const dim3 grid4(bws_grid(sp, 4));
 #define MHPC_LAUNCH_BWS(R)                                                                    \
   do {                                                                                        \
     if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
@@ -1289,7 +1301,7 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
 // Whether the sweep runs as an SRB launch beside the partials and a WB launch after them:
 // both kinds of phase present, not switched off (var_overlap 2).
 bool bws_split(const SolveParams& sp) {
-  return sp.n_wb > 0 && sp.P > sp.n_wb && sp.var_overlap != 2;
+  return sp.split_ok && sp.var_overlap != 2;
 }
 
 }  // namespace MHPC_NS

@@ -125,12 +125,31 @@ extern "C" int mhpc_rollout_costs(mhpc_handle* h, int n_eps, const double* eps, 
   FWD(rollout_costs, n_eps, eps, J, viol, ms);
 }
 extern "C" int mhpc_get_cost_gradients(mhpc_handle* h, int phase, double* lx, double* Phix) {
-  FWD(get_cost_gradients, phase, lx, Phix);
+  int B = 0;
+  if (h) B = h->precision == 32 ? mhpc32::api_batch((mhpc32::Handle*)h->impl)
+                                : mhpc::api_batch((mhpc::Handle*)h->impl);
+  FWD(get_cost_gradients, phase, 0, B, lx, Phix);
+}
+extern "C" int mhpc_get_cost_gradients_problems(mhpc_handle* h, int phase, int first, int count,
+                                                double* lx, double* Phix) {
+  FWD(get_cost_gradients, phase, first, count, lx, Phix);
 }
 extern "C" int mhpc_update_problem(mhpc_handle* h, const mhpc_gait* gait) {
   FWD(update_problem, gait);
 }
 extern "C" int mhpc_get_desc(mhpc_handle* h, mhpc_problem_desc* desc) { FWD(get_desc, desc); }
+extern "C" int mhpc_update_problems(mhpc_handle* h, int n_gaits, const mhpc_gait* gaits,
+                                    const int32_t* gait_of_problem, const int32_t* steps) {
+  FWD(update_problems, n_gaits, gaits, gait_of_problem, steps);
+}
+extern "C" int mhpc_set_layouts(mhpc_handle* h, int n_desc, const mhpc_problem_desc* descs,
+                                const int32_t* layout_of_problem) {
+  FWD(set_layouts, n_desc, descs, layout_of_problem);
+}
+extern "C" int mhpc_get_problem_desc(mhpc_handle* h, int problem, mhpc_problem_desc* desc) {
+  FWD(get_problem_desc, problem, desc);
+}
+extern "C" int mhpc_num_layouts(mhpc_handle* h, int* n) { FWD(num_layouts, n); }
 extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) { FWD(get_counters, c); }
 extern "C" int mhpc_set_profiling(mhpc_handle* h, int on) { FWD(set_profiling, on); }
 extern "C" int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches,

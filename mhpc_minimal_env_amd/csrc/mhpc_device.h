@@ -28,6 +28,53 @@ static __device__ __forceinline__ real* traj_ptr(const SolveParams& sp, const De
 
 static __device__ __forceinline__ int ntc_of(int mode, bool wb) { return wb && (mode == 2 || mode == 4); }
 
+// ---- layout groups ----------------------------------------------------------------------
+// A launch over the batch enumerates its blocks group by group: group g (problems
+// gidx[go[g] .. go[g+1]), layout g) takes ceil(n_g / per) blocks of `per` problems, so every
+// wave of a block runs one layout (uniform control flow, the layout in scalar registers).
+struct GrpBlk {
+  int g;       // layout group (-1: block past the last group)
+  int p0, p1;  // the block's first gidx position and the end of its group's positions
+};
+static __device__ __forceinline__ GrpBlk block_group(const SolveParams& sp, int blk, int per) {
+  int start = 0;
+  for (int g = 0; g < sp.ngrp; ++g) {
+    const int n = sp.go[g + 1] - sp.go[g], nb = (n + per - 1) / per;
+    if (blk < start + nb) return {g, sp.go[g] + (blk - start) * per, sp.go[g + 1]};
+    start += nb;
+  }
+  return {-1, 0, 0};
+}
+// The same for launches of `per_item` items per problem (e.g. the partials' knots) in blocks
+// of `nt` lanes: group g takes ceil(n_g * items_g / nt) blocks; *t0 = the block's first item
+// of the group (problem position go[g] + item / items_g).
+// (items == nullptr: n_items for every group)
+static __device__ __forceinline__ int block_group_items(const SolveParams& sp, const int* items,
+                                                         int n_items, int blk, int nt, long* t0) {
+  int start = 0;
+  for (int g = 0; g < sp.ngrp; ++g) {
+    const long n = (long)(sp.go[g + 1] - sp.go[g]) * (items ? items[g] : n_items);
+    const int nb = (int)((n + nt - 1) / nt);
+    if (blk < start + nb) {
+      *t0 = (long)(blk - start) * nt;
+      return g;
+    }
+    start += nb;
+  }
+  return -1;
+}
+// Problem index at gidx position pos.
+static __device__ __forceinline__ int prob_at(const SolveParams& sp, const DevBufs& d, int pos) {
+  return sp.ident ? pos : d.gidx[pos];
+}
+// Layout g, read through the constant address space: the table never changes during a launch,
+// so every field a wave-uniform index selects is a scalar load (s_load), as a parameter-block
+// field would be, never a vector load plus readfirstlane.
+typedef const __attribute__((address_space(4))) Layout CLayout;
+static __device__ __forceinline__ const Layout& layout_of(const DevBufs& d, int g) {
+  return *(const Layout*)((CLayout*)d.lay + g);
+}
+
 // Natural log of a positive argument (the barrier's g > delta > 0 and delta itself).  fp64:
 // the fdlibm algorithm (e_log.c: x = 2^k (1 + f) with sqrt(2)/2 <= 1 + f < sqrt(2),
 // s = f / (2 + f), a degree-14 odd polynomial in s), < 1 ulp -- about a third of the

@@ -94,7 +94,6 @@ constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
 typedef real sreal2 __attribute__((ext_vector_type(2)));
 constexpr int ST_PPW = 6;      // problems per staged wave (64 lanes / 10 candidates)
 constexpr int ST_PAIRS = 193;   // staged pairs per problem (192 + 1: problems on distinct LDS banks)
-constexpr int ST_RMAX = 128;    // staged position references per problem (knots per phase)
 
 // Line-search staging (ST): the 10 candidates of a problem share its nominal, gains and
 // references, so each wave loads them once per problem, cooperatively, one chunk of CH
@@ -141,16 +140,17 @@ __device__ __forceinline__ StageLane stage_lane(int lane) {
   return L;
 }
 
-// Issue the loads of chunk [k0, k0 + CH) of phase (ko, nr rollout knots) into pf.  Every
-// load is unconditional (lanes without an item re-read the chunk base, absent problems
-// problem 0's): a masked load would merge with the register's old value and make the
+// Issue the loads of chunk [k0, k0 + CH) of phase (ko, nr rollout knots) into pf (pbv: the
+// problem of each staged slot).  Every load is unconditional (lanes without an item re-read
+// the chunk base, absent problems problem 0's): a masked load would merge with the register's old value and make the
 // compiler wait for it on the spot, which is exactly the round trip the stage hides.
 // NP: problem slots of the wave (ST_PPW; 3 in the pair variant, whose dynamics wave holds
 // 3 problems x 10 candidates) -- slots past NP would only load problem 0's data again.
 template <bool WB, int NP>
 __device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs& d,
-                                            const StageLane& L, int b0, int ko, int k0, int nr,
-                                            const int (&nomv)[ST_PPW], sreal2 (&pf)[ST_PPW * 3]) {
+                                            const StageLane& L, const int (&pbv)[ST_PPW], int ko,
+                                            int k0, int nr, const int (&nomv)[ST_PPW],
+                                            sreal2 (&pf)[ST_PPW * 3]) {
   const int lim = nr - k0;  // chunk knots that exist
   const int oA = L.kcA < lim ? L.offA : 0;
   const int oB = L.kcB >= 0 && L.kcB < lim ? L.offB : 0;
@@ -158,7 +158,7 @@ __device__ __forceinline__ void stage_issue(const SolveParams& sp, const DevBufs
 #pragma unroll
   for (int lp = 0; lp < NP; ++lp) {
     const int nom = nomv[lp];  // < 0: problem absent or not iterating (uniform)
-    const int bb = nom >= 0 ? b0 + lp : 0;
+    const int bb = nom >= 0 ? pbv[lp] : 0;
     const size_t kk = (size_t)bb * sp.NK + ko + k0;
     const real* Kb = d.K + kk * 56;
     const real* Tb = traj_ptr(sp, d, bb, nom >= 0 ? nom : 0, ko + k0);
@@ -217,8 +217,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   const int cl = (PAIR && w0) ? (lane >> 1) : lane;
   const bool back = PAIR && (lane & 1);  // the dynamics lane's leg
   const int lp = cl / nc, j = cl - lp * nc;
-  const int b = blockIdx.x * ppw + lp;
-  const bool in = lp < ppw && b < sp.B;
+  // the block's layout group and problems (a block never mixes layouts)
+  const GrpBlk gb = block_group(sp, blockIdx.x, ppw);
+  if (gb.g < 0) return;  // (uniform; the grid has no such block)
+  const Layout& L = layout_of(d, gb.g);
+  const bool in = lp < ppw && gb.p0 + lp < gb.p1;
+  const int b = in ? prob_at(sp, d, gb.p0 + lp) : 0;
 
   // ring of RD knot records; the waves meet at a barrier every RD / 2 records
   constexpr int RD = PIPE ? (PAIR ? RO_RING_PAIR : 2) : 1;
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   __shared__ acc sJ[64], sViol[64], sV[MAXP][64];
   __shared__ real sH[MAXP][64];
   __shared__ int sAny;
-  __shared__ int sNom[ST ? ST_PPW : 1];
+  __shared__ int sNom[ST ? ST_PPW : 1], sProb[ST ? ST_PPW : 1];
   __shared__ sreal2 stage2[ST ? SNP * ST_PAIRS : 1];
   __shared__ real sRef[ST ? SNP : 1][ST ? ST_RMAX + 1 : 1];  // +1: distinct banks
 #ifdef MHPC_RO_TIMING
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 #endif
 
   if (t == 0) sAny = 0;
-  if (ST && t < ST_PPW) sNom[t] = -1;
+  if (ST && t < ST_PPW) { sNom[t] = -1; sProb[t] = 0; }
   __syncthreads();
   bool run = false;
   int nom = 0, slot = 0;
@@ -254,11 +258,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     }
   }
   if (w0 && run) sAny = 1;
-  if (ST && w0 && run && j == 0) sNom[lp] = nom;
+  if (ST && w0 && run && j == 0) { sNom[lp] = nom; sProb[lp] = b; }
   __syncthreads();
   int nomv[ST_PPW];  // nominal slot of each staged problem, -1 if absent / not iterating
+  int pbv[ST_PPW];   // its problem index
 #pragma unroll
-  for (int i = 0; i < ST_PPW; ++i) nomv[i] = ST ? __builtin_amdgcn_readfirstlane(sNom[i]) : -1;
+  for (int i = 0; i < ST_PPW; ++i) {
+    nomv[i] = ST ? __builtin_amdgcn_readfirstlane(sNom[i]) : -1;
+    pbv[i] = ST ? __builtin_amdgcn_readfirstlane(sProb[i]) : 0;
+  }
   if (!sAny) return;  // uniform: no problem of this block is still iterating
   if (full == 1 && run && w0) {  // top of the AL iteration (MultiPhaseDDP.cpp:172-190)
     if (al_iter == 1) { st->cap_reb = st->opt_reb; st->cap_pen = st->opt_pen; }
@@ -294,7 +302,6 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     for (int i = 0; i < RING_W / 2; ++i)
       if (2 * i < n) o[i] = real2{r[2 * i], r[2 * i + 1]};
   };
-  const int b0 = blockIdx.x * ppw;
   real f[4] = {0, 0, 0, 0}, sc[2] = {0, 0};  // SRB phase: foothold, contact flags
   sreal2 pf[ST_PPW * 3];                    // the next chunk's stage loads in flight
   // PF (pair variant): the feedback operands of knot k+1 (own K rows, nominal x / u, du) are
@@ -337,22 +344,25 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     stage_drop<SNP>(lane, pf, stage2);
     if (k1 + CH < N - 1) {
       const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
-      if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, k1 + CH, N - 1, nomv, pf);
-      else stage_issue<false, SNP>(sp, d, SL, b0, ko, k1 + CH, N - 1, nomv, pf);
+      if (wb) stage_issue<true, SNP>(sp, d, SL, pbv, ko, k1 + CH, N - 1, nomv, pf);
+      else stage_issue<false, SNP>(sp, d, SL, pbv, ko, k1 + CH, N - 1, nomv, pf);
     }
   };
   // dynamics side, phase start: SRB foothold / contact, first chunk of the stage
-  auto dyn_phase_begin = [&](int p) __attribute__((always_inline)) {
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const bool wb = p < sp.n_wb;
+  // (the phase kind WBc is a compile-time argument of every per-phase / per-knot helper: each
+  // knot loop is specialised per kind, and a run-time p < n_wb here would make the compiler
+  // keep both kinds' code inside each loop)
+  auto dyn_phase_begin = [&](auto WBc, int p) __attribute__((always_inline)) {
+    const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
+    constexpr bool wb = decltype(WBc)::value;
     if (run && !wb) {
-      plan_foothold(x, sp.dt[p] * N, mode, f);
+      plan_foothold(x, L.dt[p] * N, mode, f);
       srb_contact(mode, sc);
     }
     if (ST) {
       const StageLane SL = wb ? stage_lane<true>(lane) : stage_lane<false>(lane);
-      if (wb) stage_issue<true, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
-      else stage_issue<false, SNP>(sp, d, SL, b0, ko, 0, N - 1, nomv, pf);
+      if (wb) stage_issue<true, SNP>(sp, d, SL, pbv, ko, 0, N - 1, nomv, pf);
+      else stage_issue<false, SNP>(sp, d, SL, pbv, ko, 0, N - 1, nomv, pf);
     }
     if (PF) {
       chunk_turn(wb, ko, N, 0);
@@ -361,10 +371,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // dynamics side, knot k of phase p: u = (u_nom + eps du) + K (x - x_nom), x+ = x + dt f(x, u);
   // rr = the knot's record (x, u, y) as the ring / the cost side takes it
-  auto dyn_knot = [&](int p, int k, real* rr) __attribute__((always_inline)) {
-    const int mode = sp.mode[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
-    const bool wb = p < sp.n_wb;
+  auto dyn_knot = [&](auto WBc, int p, int k, real* rr) __attribute__((always_inline)) {
+    const int mode = L.mode[p], ko = L.ko[p];
+    const real dt = L.dt[p];
+    constexpr bool wb = decltype(WBc)::value;
     const int kc = k & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
     const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
     const int D0 = wb ? Stage<true>::D0 : Stage<false>::D0;
@@ -436,15 +446,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     }
   };
   // phase transition after the phase's terminal state (MultiPhaseDDP.cpp:351-379)
-  auto transition = [&](int p) __attribute__((always_inline)) {
-    const int mode = sp.mode[p];
-    if (p < sp.n_wb && p + 1 < sp.P) {
+  auto transition = [&](auto WBc, int p) __attribute__((always_inline)) {
+    const int mode = L.mode[p];
+    if (decltype(WBc)::value && p + 1 < L.P) {
       if (mode == 2 || mode == 4) {
         real xp[14], lam[2];
         wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
         for (int i = 0; i < 14; ++i) x[i] = xp[i];
       }
-      if (p + 1 >= sp.n_wb) {
+      if (p + 1 >= L.n_wb) {
         const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
         x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
       }
@@ -464,13 +474,13 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 #pragma unroll
     for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
       const int fi = lane + 64 * i, rl = fi / ST_RMAX, rk = fi - rl * ST_RMAX;
-      if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)(b0 + rl) * sp.NK + ko + rk];
+      if (rk < N && sNom[rl] >= 0) sRef[rl][rk] = d.refpos[(size_t)sProb[rl] * sp.NK + ko + rk];
     }
   };
-  auto cost_phase_begin = [&](int p) __attribute__((always_inline)) {
+  auto cost_phase_begin = [&](auto WBc, int p) __attribute__((always_inline)) {
     CostPhase c;
-    const int N = sp.N[p], ko = sp.ko[p];
-    const bool wb = p < sp.n_wb;
+    const int N = L.N[p], ko = L.ko[p];
+    constexpr bool wb = decltype(WBc)::value;
     c.delta = c.etq = c.egr = real(0.0);
     if (run && wb) { c.delta = st->delta[p]; c.etq = st->eps_tq[p]; c.egr = st->eps_grf[p]; }
     c.refpos = (const __attribute__((address_space(1))) real*)(d.refpos + (size_t)(in ? b : 0) * sp.NK + ko);
@@ -480,11 +490,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // cost side: the running cost of knot kk from record r (knot order: the serial rollout's
   // association) and the record's store
-  auto cost_knot = [&](int p, const CostPhase& c, int kk, const real* r, acc& V) __attribute__((always_inline)) {
+  auto cost_knot = [&](auto WBc, int p, const CostPhase& c, int kk, const real* r, acc& V) __attribute__((always_inline)) {
     MHPC_NO_FMA_COST
-    const int mode = sp.mode[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
-    const bool wb = p < sp.n_wb;
+    const int mode = L.mode[p], ko = L.ko[p];
+    const real dt = L.dt[p];
+    constexpr bool wb = decltype(WBc)::value;
     const real pos = ST ? sRef[lp][kk] : c.refpos[kk];
     if (full != 2)  // (a re-roll only writes the records)
       V += wb ? wb_running_cost(sp, mode, dt, pos, r, r + 14, r + 18, reb, c.delta, c.etq, c.egr)
@@ -497,10 +507,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // cost side, phase end: terminal cost, touchdown constraint, AL term (SinglePhase.cpp
   // :251-275), the phase value into sV / sH and the terminal record's store
-  auto cost_terminal = [&](int p, const CostPhase& c, const real* xe, acc V) __attribute__((always_inline)) {
+  auto cost_terminal = [&](auto WBc, int p, const CostPhase& c, const real* xe, acc V) __attribute__((always_inline)) {
     MHPC_NO_FMA_COST
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const bool wb = p < sp.n_wb;
+    const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
+    constexpr bool wb = decltype(WBc)::value;
     if (full == 2) {
       store_rec(xe, wb ? 14 : 6, ko + N - 1, false);
       return;
@@ -546,9 +556,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       // registers inside the loop (those forced the prefetched operands to land early)
       auto dyn_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
         constexpr bool wb = decltype(WBc)::value;
-        const int N = sp.N[p], ko = sp.ko[p];
+        const int N = L.N[p], ko = L.ko[p];
         constexpr int nx = wb ? 14 : 6;
-        dyn_phase_begin(p);
+        dyn_phase_begin(WBc, p);
         for (int k = 0; k < N - 1; ++k, ++q) {
           const int s = q & (RD - 1);
           const bool bar = (q & (RG - 1)) == RG - 1;
@@ -557,7 +567,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           RO_T(tk0);
           if (ST && !PF && (k & (CH - 1)) == 0) chunk_turn(wb, ko, N, k);
           RO_T(tkc);
-          if (run) dyn_knot(p, k, rr);
+          if (run) dyn_knot(WBc, p, k, rr);
           RO_T(tk2);
           if (PF && k + 1 < N - 1) {
             if (((k + 1) & (CH - 1)) == 0) chunk_turn(wb, ko, N, k + 1);
@@ -607,20 +617,20 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           } else {
             for (int i = 0; i < nx; ++i) ring[s][i][lane] = x[i];
           }
-          transition(p);
+          transition(WBc, p);
         }
         __syncthreads();
       };
-      for (int p = 0; p < sp.P; ++p) {
-        if (p < sp.n_wb) dyn_phase(std::true_type{}, p);
+      for (int p = 0; p < L.P; ++p) {
+        if (p < L.n_wb) dyn_phase(std::true_type{}, p);
         else dyn_phase(std::false_type{}, p);
       }
     } else {
       auto cost_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
         constexpr bool wb = decltype(WBc)::value;
-        const int N = sp.N[p];
+        const int N = L.N[p];
         constexpr int nrec = wb ? RING_W : 14;
-        const CostPhase c = cost_phase_begin(p);
+        const CostPhase c = cost_phase_begin(WBc, p);
         acc V = 0;
         int pend = -1;  // a knot record handed over but not consumed yet (RG > 1)
         for (int k = 0; k < N - 1; ++k, ++q) {
@@ -638,10 +648,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
               real r[RING_W];
               if (RG > 1 && pend >= 0) {
                 ring_rec((s - 1) & (RD - 1), r, nrec);
-                cost_knot(p, c, pend, r, V);
+                cost_knot(WBc, p, c, pend, r, V);
               }
               ring_rec(s, r, nrec);
-              cost_knot(p, c, k, r, V);
+              cost_knot(WBc, p, c, k, r, V);
             }
 #ifdef MHPC_RO_TIMING
             if (lane == 0 && run) {  // cost wave: barrier wait, consume time per WB / SRB record
@@ -660,14 +670,14 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           real r[RING_W];
           if (RG > 1 && pend >= 0) {  // the phase's last knot record, if still waiting
             ring_rec((s - 1) & (RD - 1), r, nrec);
-            cost_knot(p, c, N - 2, r, V);
+            cost_knot(WBc, p, c, N - 2, r, V);
           }
           ring_rec(s, r, wb ? 14 : 6);
-          cost_terminal(p, c, r, V);
+          cost_terminal(WBc, p, c, r, V);
         }
       };
-      for (int p = 0; p < sp.P; ++p) {
-        if (p < sp.n_wb) cost_phase(std::true_type{}, p);
+      for (int p = 0; p < L.P; ++p) {
+        if (p < L.n_wb) cost_phase(std::true_type{}, p);
         else cost_phase(std::false_type{}, p);
       }
     }
@@ -676,33 +686,33 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     // copy of the knot loop per phase kind
     auto fused_phase = [&](auto WBc, int p) __attribute__((always_inline)) {
       constexpr bool wb = decltype(WBc)::value;
-      const int N = sp.N[p], ko = sp.ko[p];
+      const int N = L.N[p], ko = L.ko[p];
       constexpr int CH = wb ? Stage<true>::CH : Stage<false>::CH;
-      dyn_phase_begin(p);
-      const CostPhase c = cost_phase_begin(p);
+      dyn_phase_begin(WBc, p);
+      const CostPhase c = cost_phase_begin(WBc, p);
       acc V = 0;
       for (int k = 0; k < N - 1; ++k) {
         if (ST && (k & (CH - 1)) == 0) chunk_turn(wb, ko, N, k);
         if (run) {
           real rr[RING_W];
-          dyn_knot(p, k, rr);
+          dyn_knot(WBc, p, k, rr);
           if (!wb) {
 #pragma unroll
             for (int i = 6; i < RING_W; ++i) rr[i] = i < 14 ? rr[i] : real(0.0);
           }
-          cost_knot(p, c, k, rr, V);
+          cost_knot(WBc, p, c, k, rr, V);
         }
       }
       if (run) {
         real xe[RING_W];
 #pragma unroll
         for (int i = 0; i < RING_W; ++i) xe[i] = i < (wb ? 14 : 6) ? x[i] : real(0.0);
-        transition(p);
-        cost_terminal(p, c, xe, V);
+        transition(WBc, p);
+        cost_terminal(WBc, p, c, xe, V);
       }
     };
-    for (int p = 0; p < sp.P; ++p) {
-      if (p < sp.n_wb) fused_phase(std::true_type{}, p);
+    for (int p = 0; p < L.P; ++p) {
+      if (p < L.n_wb) fused_phase(std::true_type{}, p);
       else fused_phase(std::false_type{}, p);
     }
   }
@@ -723,12 +733,12 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     if (w1 && run) {
       st->J = J;
       st->viol = sqrt(viol2);
-      for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][lane]; st->h[p] = sH[p][lane]; }
+      for (int p = 0; p < L.P; ++p) { st->V[p] = sV[p][lane]; st->h[p] = sH[p][lane]; }
       st->nom_slot = slot;
       st->par_slot = slot;
       st->par_al = sp.AL_active ? 1 : 0;
       st->ls_nt = 0;
-      for (int p = 0; p < sp.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
+      for (int p = 0; p < L.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
       st->al_iter = al_iter;
       st->reg = 0;
       st->ddp_active = 1;
@@ -752,7 +762,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     st->reroll_eps = sp.eps[sel];
     st->J = sJ[sl];
     st->viol = sViol[sl];
-    for (int p = 0; p < sp.P; ++p) { st->V[p] = sV[p][sl]; st->h[p] = sH[p][sl]; }
+    for (int p = 0; p < L.P; ++p) { st->V[p] = sV[p][sl]; st->h[p] = sH[p][sl]; }
     st->nom_slot = sel < nom ? sel : sel + 1;
     const bool conv = cost_prev - st->J < sp.DDP_thresh;
     if (st->ntrace < TRACE)
@@ -765,7 +775,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       st->ddp_active = 0;
       st->ls_nt = nls < nc ? nls : nc;  // trials whose AL terms stay in Phix (see ProbState)
       st->ls_nom = nom;
-      for (int p = 0; p < sp.P; ++p) { st->ls_sigma[p] = st->sigma[p]; st->ls_lambda[p] = st->lambda[p]; }
+      for (int p = 0; p < L.P; ++p) { st->ls_sigma[p] = st->sigma[p]; st->ls_lambda[p] = st->lambda[p]; }
     } else {
       st->cnt[C_PAR]++;
       st->al_partials = 0;
@@ -787,9 +797,16 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, int n_eps,
                                                     const real* eps_v, real* Jo,
                                                     real* vo) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)sp.B * n_eps) return;
-  const int b = (int)(t / n_eps), e = (int)(t - (long)b * n_eps);
+  // blocks by layout group, lanes = (problem of the group, step size)
+  long t0 = 0;
+  const int g = block_group_items(sp, nullptr, n_eps, blockIdx.x, 64, &t0);
+  if (g < 0) return;
+  const Layout& L = layout_of(d, g);
+  const long tg = t0 + threadIdx.x;  // item within the group
+  if (tg >= (long)(sp.go[g + 1] - sp.go[g]) * n_eps) return;
+  const int pos = sp.go[g] + (int)(tg / n_eps), e = (int)(tg % n_eps);
+  const int b = prob_at(sp, d, pos);
+  const long t = (long)b * n_eps + e;  // output index [problem][step size]
   const ProbState* st = &d.st[b];
   const int nom = st->nom_slot;
   const real eps = eps_v[e];
@@ -798,13 +815,13 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
   const real* x0 = d.x0 + (size_t)b * 14;
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
   acc J = 0, viol2 = 0;
-  for (int p = 0; p < sp.P; ++p) {
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
+  for (int p = 0; p < L.P; ++p) {
+    const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
+    const real dt = L.dt[p];
     const real* refpos = d.refpos + (size_t)b * sp.NK + ko;
     acc V = 0;
     real h = 0;
-    if (p < sp.n_wb) {
+    if (p < L.n_wb) {
       const real delta = st->delta[p], etq = st->eps_tq[p], egr = st->eps_grf[p];
       for (int k = 0; k < N - 1; ++k) {
         const real* nk = traj_ptr(sp, d, b, nom, ko + k);
@@ -839,13 +856,13 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
         }
         V += Phi;
       }
-      if (p + 1 < sp.P) {
+      if (p + 1 < L.P) {
         if (mode == 2 || mode == 4) {
           real xp[14], lam[2];
           wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
           for (int i = 0; i < 14; ++i) x[i] = xp[i];
         }
-        if (p + 1 >= sp.n_wb) {
+        if (p + 1 >= L.n_wb) {
           const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
           x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
         }
@@ -889,21 +906,23 @@ __global__ __launch_bounds__(64) void k_eps_rollout(SolveParams sp, DevBufs d, i
 // CostBase.cpp:19-31,49-60 + the AL term of SinglePhase.cpp:257-275 when it was a
 // forward_sweep(0)), for print_debugInfo's cost.txt.  The constraint terms added to lx are
 // exact zeros (joint limits carry eps_ReB = 0; torque / GRF limits do not depend on x).
-// Lane = (problem, knot); lx [B][N-1][n], phix [B][n].
+// Problems [b0, b0 + nb), all of layout g; lane = (problem, knot); lx [nb][N-1][n], phix [nb][n].
 // ============================================================================================
-__global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* phix) {
-  const int N = sp.N[p], ko = sp.ko[p], mode = sp.mode[p];
+__global__ void k_cost_grad(SolveParams sp, DevBufs d, int g, int p, int b0, int nb, real* lx,
+                            real* phix) {
+  const Layout& L = layout_of(d, g);
+  const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)sp.B * N) return;
-  const int b = (int)(t / N), k = (int)(t - (long)b * N);
+  if (t >= (long)nb * N) return;
+  const int i0 = (int)(t / N), k = (int)(t - (long)i0 * N), b = b0 + i0;
   const ProbState* st = &d.st[b];
-  const bool wb = p < sp.n_wb;
+  const bool wb = p < L.n_wb;
   const int n = wb ? 14 : 6;
-  const real dt = sp.dt[p];
+  const real dt = L.dt[p];
   const real* x = traj_ptr(sp, d, b, st->par_slot, ko + k);
   const real pos = d.refpos[(size_t)b * sp.NK + ko + k];
   if (k < N - 1) {
-    real* o = lx + ((size_t)b * (N - 1) + k) * n;
+    real* o = lx + ((size_t)i0 * (N - 1) + k) * n;
     for (int i = 0; i < n; ++i) {
       real rxi, w2;
       if (wb) {
@@ -917,7 +936,7 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* ph
       o[i] = w2 * (x[i] - rxi);
     }
   } else {
-    real* o = phix + (size_t)b * n;
+    real* o = phix + (size_t)i0 * n;
     if (wb) {
       real rx[14];
       wb_term_ref(sp, mode, pos, rx);
@@ -957,19 +976,22 @@ __global__ void k_cost_grad(SolveParams sp, DevBufs d, int p, real* lx, real* ph
 // Phase buffers of the receding-horizon loop (MHPCLocomotion::update_problem,
 // MHPCLocomotion.cpp:107-158): the reference keeps one N_TIMESTEPS_MAX-knot buffer per WB
 // and per SRB phase slot (nominal x,u,y and cost-to-go) and rotates which buffer each phase
-// uses.  store [B][P][nbk][SREC]: x,u,y (a traj record), K 56, du 4, G 14.  Phase p of the
-// current layout lives in buffer sp.buf[p].
+// uses.  store [B][spmax][nbk][SREC]: x,u,y (a traj record), K 56, du 4, G 14.  Phase p of a
+// problem's layout lives in its buffer L.buf[p]; k_store_save runs with the layouts before
+// an update, k_store_load with those after it.
 // ============================================================================================
 constexpr int SREC = KS + 56 + 4 + 14;
 
-__global__ void k_store_save(SolveParams sp, DevBufs d, real* store, int nbk) {
+__global__ void k_store_save(SolveParams sp, DevBufs d, real* store, int nbk, int spmax) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * sp.NK) return;
   const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
+  const Layout& L = d.lay[d.lid[b]];  // the problem's layout (per lane: not a hot kernel)
+  if (kk >= L.NK) return;
   int p = 0;
-  while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
-  const int k = kk - sp.ko[p];
-  real* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  while (p + 1 < L.P && kk >= L.ko[p + 1]) ++p;
+  const int k = kk - L.ko[p];
+  real* o = store + (((size_t)b * spmax + L.buf[p]) * nbk + k) * SREC;
   const real* r = traj_ptr(sp, d, b, d.st[b].nom_slot, kk);
   for (int i = 0; i < KS; ++i) o[i] = r[i];
   const size_t rec = (size_t)b * sp.NK + kk;
@@ -978,17 +1000,19 @@ __global__ void k_store_save(SolveParams sp, DevBufs d, real* store, int nbk) {
   for (int i = 0; i < 14; ++i) o[KS + 60 + i] = d.G[rec * 14 + i];
 }
 
-__global__ void k_store_load(SolveParams sp, DevBufs d, const real* store, int nbk) {
+__global__ void k_store_load(SolveParams sp, DevBufs d, const real* store, int nbk, int spmax) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)sp.B * sp.NK) return;
   const int b = (int)(t / sp.NK), kk = (int)(t - (long)b * sp.NK);
+  const Layout& L = d.lay[d.lid[b]];  // the problem's layout (per lane: not a hot kernel)
+  if (kk >= L.NK) return;
   int p = 0;
-  while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
-  const int k = kk - sp.ko[p];
-  const real* o = store + (((size_t)b * sp.P + sp.buf[p]) * nbk + k) * SREC;
+  while (p + 1 < L.P && kk >= L.ko[p + 1]) ++p;
+  const int k = kk - L.ko[p];
+  const real* o = store + (((size_t)b * spmax + L.buf[p]) * nbk + k) * SREC;
   real* r = traj_ptr(sp, d, b, 0, kk);  // k_init(warm = 0) sets nom_slot = 0
   for (int i = 0; i < KS; ++i) r[i] = o[i];
-  if (k == sp.N[p] - 1)  // u, y of the last knot are never rewritten by a sweep (B11): the
+  if (k == L.N[p] - 1)  // u, y of the last knot are never rewritten by a sweep (B11): the
     for (int sl = 1; sl < sp.nslot; ++sl) {  // buffer's stale tail must follow any trial
       real* q = traj_ptr(sp, d, b, sl, kk);
       for (int i = 0; i < KS; ++i) q[i] = o[i];
@@ -999,15 +1023,15 @@ __global__ void k_store_load(SolveParams sp, DevBufs d, const real* store, int n
   for (int i = 0; i < 14; ++i) d.G[rec * 14 + i] = o[KS + 60 + i];
 }
 
-hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, int nbk, int save,
-                        hipStream_t s) {
+hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, int nbk, int spmax,
+                        int save, hipStream_t s) {
   const long n = (long)sp.B * sp.NK;
   if (save)
     hipLaunchKernelGGL(k_store_save, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d,
-                       store, nbk);
+                       store, nbk, spmax);
   else
     hipLaunchKernelGGL(k_store_load, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d,
-                       store, nbk);
+                       store, nbk, spmax);
   return hipGetLastError();
 }
 
@@ -1080,16 +1104,22 @@ __device__ __forceinline__ void partials_knot(const real* nk, real* rec) {
 #endif
 template <int G>
 __global__ __launch_bounds__(MHPC_PAR_BLOCK, MHPC_PAR_MINB) void k_partials(SolveParams sp, DevBufs d) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = (int)(t / sp.par_knots);
-  if (b >= sp.B) return;
-  const int it = (int)(t - (long)b * sp.par_knots);
+  // blocks by layout group, lanes = (problem of the group, WB knot)
+  long t0 = 0;
+  const int g = block_group_items(sp, sp.gpk, 0, blockIdx.x, MHPC_PAR_BLOCK, &t0);
+  if (g < 0) return;
+  const Layout& L = layout_of(d, g);
+  const long t = t0 + threadIdx.x;
+  const int i0 = (int)(t / L.par_knots);
+  if (i0 >= sp.go[g + 1] - sp.go[g]) return;
+  const int it = (int)(t - (long)i0 * L.par_knots);
+  const int b = prob_at(sp, d, sp.go[g] + i0);
   const ProbState* st = &d.st[b];
   if (!(st->active && st->ddp_active)) return;
   int p = 0;
-  while (it >= sp.par_knot_off[p + 1]) ++p;
-  const int k = it - sp.par_knot_off[p];
-  const int ko = sp.ko[p], mode = sp.mode[p];
+  while (it >= L.par_knot_off[p + 1]) ++p;
+  const int k = it - L.par_knot_off[p];
+  const int ko = L.ko[p], mode = L.mode[p];
   const real* nk = traj_ptr(sp, d, b, st->nom_slot, ko + k);
   real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
   if (mode == 1) partials_knot<kBack, G>(nk, rec);
@@ -1099,7 +1129,7 @@ __global__ __launch_bounds__(MHPC_PAR_BLOCK, MHPC_PAR_MINB) void k_partials(Solv
     // running-cost derivatives of controls and contact forces at the nominal knot
     // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
     real c[14];
-    wb_cost_uy_derivs(sp, mode, sp.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
+    wb_cost_uy_derivs(sp, mode, L.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
                       st->eps_tq[p], st->eps_grf[p], c);
 #pragma unroll
     for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
@@ -1107,17 +1137,22 @@ __global__ __launch_bounds__(MHPC_PAR_BLOCK, MHPC_PAR_MINB) void k_partials(Solv
 }
 
 __global__ __launch_bounds__(256) void k_partials_impact(SolveParams sp, DevBufs d) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = (int)(t / sp.par_imp);
-  if (b >= sp.B) return;
-  const int it = (int)(t - (long)b * sp.par_imp);
+  long t0 = 0;
+  const int g = block_group_items(sp, sp.gpi, 0, blockIdx.x, 256, &t0);
+  if (g < 0) return;
+  const Layout& L = layout_of(d, g);
+  const long t = t0 + threadIdx.x;
+  const int i0 = (int)(t / L.par_imp);
+  if (i0 >= sp.go[g + 1] - sp.go[g]) return;
+  const int it = (int)(t - (long)i0 * L.par_imp);
+  const int b = prob_at(sp, d, sp.go[g] + i0);
   const ProbState* st = &d.st[b];
   if (!(st->active && st->ddp_active)) return;
   int p = 0;
-  while (it >= sp.par_imp_off[p + 1]) ++p;
-  const int dir = it - sp.par_imp_off[p];
-  const int mode = sp.mode[p];
-  const real* nk = traj_ptr(sp, d, b, st->nom_slot, sp.ko[p] + sp.N[p] - 1);
+  while (it >= L.par_imp_off[p + 1]) ++p;
+  const int dir = it - L.par_imp_off[p];
+  const int mode = L.mode[p];
+  const real* nk = traj_ptr(sp, d, b, st->nom_slot, L.ko[p] + L.N[p] - 1);
   Dual x[14], xp[14], lam[2];
 #pragma unroll
   for (int i = 0; i < 14; ++i) x[i] = Dual(nk[i], i == dir ? real(1.0) : real(0.0));
@@ -1131,20 +1166,22 @@ __global__ __launch_bounds__(256) void k_partials_impact(SolveParams sp, DevBufs
 // AL / ReB update (MultiPhaseDDP.cpp:273-284, SinglePhase.cpp:334-354)
 // ============================================================================================
 __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= sp.B) return;
+  const GrpBlk gb = block_group(sp, blockIdx.x, 64);
+  if (gb.g < 0 || gb.p0 + (int)threadIdx.x >= gb.p1) return;
+  const Layout& L = layout_of(d, gb.g);
+  const int b = prob_at(sp, d, gb.p0 + threadIdx.x);
   ProbState* st = &d.st[b];
   if (st->active) {
     real up = st->cap_pen;  // _option.update_penalty = captured value, 0 if satisfied
     if (st->viol < real(0.03)) up = 0;
     st->opt_pen = up;
-    for (int p = 0; p < sp.P; ++p) {
-      const bool wb = p < sp.n_wb;
-      if (ntc_of(sp.mode[p], wb)) st->lambda[p] += st->sigma[p] * st->h[p];
+    for (int p = 0; p < L.P; ++p) {
+      const bool wb = p < L.n_wb;
+      if (ntc_of(L.mode[p], wb)) st->lambda[p] += st->sigma[p] * st->h[p];
       st->sigma[p] *= up;
       if (st->reb_active && wb) {
         st->delta[p] *= sp.update_relax;
-        const real dmin = sp.cw.delta_min[sp.mode[p] - 1];
+        const real dmin = sp.cw.delta_min[L.mode[p] - 1];
         if (st->delta[p] < dmin) st->delta[p] = dmin;
         st->eps_tq[p] *= sp.update_ReB;
         st->eps_grf[p] *= sp.update_ReB;
@@ -1163,22 +1200,23 @@ __global__ void k_al_end(SolveParams sp, DevBufs d, int last) {
 // every phase but keeps the (rotated) nominal trajectories and gains as the warm start.
 // References (ReferenceGen.h:94-109) and the per-problem solver state of one problem;
 // warm = 1 also resets the option fields a solve rewrites (see ProbState).
-__device__ void k_init_state(const SolveParams& sp, const DevBufs& d, int b, int warm) {
+__device__ void k_init_state(const SolveParams& sp, const DevBufs& d, const Layout& L, int b,
+                             int warm) {
   const real* x0 = d.x0 + (size_t)b * 14;
   real* pos = d.refpos + (size_t)b * sp.NK;
-  for (int p = 0; p < sp.P; ++p) {
-    const int ko = sp.ko[p];
-    pos[ko] = p == 0 ? x0[0] : pos[sp.ko[p - 1] + sp.N[p - 1] - 1];
-    for (int k = 1; k < sp.N[p]; ++k) pos[ko + k] = pos[ko + k - 1] + sp.vel * sp.dt[p];
+  for (int p = 0; p < L.P; ++p) {
+    const int ko = L.ko[p];
+    pos[ko] = p == 0 ? x0[0] : pos[L.ko[p - 1] + L.N[p - 1] - 1];
+    for (int k = 1; k < L.N[p]; ++k) pos[ko + k] = pos[ko + k - 1] + sp.vel * L.dt[p];
   }
   ProbState* st = &d.st[b];
   st->J = 0; st->viol = 0; st->dV_exp = 0; st->reg = 0; st->cost_prev = 0;
   for (int p = 0; p < MAXP; ++p) {
     st->V[p] = 0; st->dV[p] = 0; st->h[p] = 0; st->lambda[p] = 0;
-    const bool wb = p < sp.n_wb && p < sp.P;
+    const bool wb = p < L.n_wb && p < L.P;
     // AL_REB_PARAMETER of the phase's mode (MHPCConstraints.cpp:43-88, mhpc_set_constraint_params)
-    const int m = p < sp.P ? sp.mode[p] - 1 : 0;
-    st->sigma[p] = (wb && ntc_of(sp.mode[p], true)) ? sp.cw.sigma0[m] : real(0.0);
+    const int m = p < L.P ? L.mode[p] - 1 : 0;
+    st->sigma[p] = (wb && ntc_of(L.mode[p], true)) ? sp.cw.sigma0[m] : real(0.0);
     st->delta[p] = sp.cw.delta0[m];
     st->eps_tq[p] = sp.cw.eps_tq0[m];
     st->eps_grf[p] = sp.cw.eps_grf0[m];
@@ -1224,13 +1262,15 @@ __device__ void init_reset_arrays(const SolveParams& sp, const DevBufs& d, long 
   for (long i = t; i < nk * 56; i += nt) d.K[i] = real(0.0);
   for (long i = t; i < nk * 4; i += nt) d.du[i] = real(0.0);
   for (long i = t; i < nk * 14; i += nt) d.G[i] = real(0.0);
-  const long n = (long)sp.B * sp.nslot * sp.P;
+  const long n = (long)sp.B * sp.nslot * sp.pmax;
   for (long i = t; i < n; i += nt) {
-    const int p = (int)(i % sp.P);
-    const long bs = i / sp.P;
+    const int p = (int)(i % sp.pmax);
+    const long bs = i / sp.pmax;
     const int slot = (int)(bs % sp.nslot), b = (int)(bs / sp.nslot);
-    const int nx = p < sp.n_wb ? 14 : 6;
-    real* r = traj_ptr(sp, d, b, slot, sp.ko[p] + sp.N[p] - 1);
+    const Layout& L = d.lay[d.lid[b]];  // the problem's layout (per lane; hidden beside k_init)
+    if (p >= L.P) continue;
+    const int nx = p < L.n_wb ? 14 : 6;
+    real* r = traj_ptr(sp, d, b, slot, L.ko[p] + L.N[p] - 1);
     for (int e = nx; e < KS; ++e) r[e] = real(0.0);
   }
 }
@@ -1240,21 +1280,24 @@ __global__ __launch_bounds__(256) void k_reset_arrays(SolveParams sp, DevBufs d)
 }
 
 __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = t >> 1;
-  const bool back = (t & 1) != 0;
-  if (b >= sp.B) return;  // both lanes of a pair
+  // blocks by layout group, 32 problems a block
+  const GrpBlk gb = block_group(sp, blockIdx.x, 32);
+  const int i0 = threadIdx.x >> 1;
+  const bool back = (threadIdx.x & 1) != 0;
+  if (gb.g < 0 || gb.p0 + i0 >= gb.p1) return;  // both lanes of a pair
+  const Layout& L = layout_of(d, gb.g);
+  const int b = prob_at(sp, d, gb.p0 + i0);
   const real* x0 = d.x0 + (size_t)b * 14;
-  if (!back) k_init_state(sp, d, b, warm);
+  if (!back) k_init_state(sp, d, L, b, warm);
   if (!warm) return;
   // warm start of the WB phases into slot 0 (bounding_PDcontrol, boundingPDControl.cpp:3-46)
   real x[14];
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
   const real qnom[4] = {PI / 4, -PI * 7 / 12, PI / 4, -PI * 7 / 12};
   const real Kp[4] = {5 * real(8.0), 5 * real(1.0), 5 * real(12.0), 5 * real(10.0)};
-  for (int p = 0; p < sp.n_wb; ++p) {
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
+  for (int p = 0; p < L.n_wb; ++p) {
+    const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
+    const real dt = L.dt[p];
     for (int k = 0; k < N - 1; ++k) {
       real u[4];
       if (mode == 1 || mode == 3) {
@@ -1284,13 +1327,13 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
     real* oe = traj_ptr(sp, d, b, 0, ko + N - 1);
     if (!back) for (int i = 0; i < 14; ++i) oe[i] = x[i];
     // phase transition exactly as the forward sweep does it (MultiPhaseDDP.cpp:351-379)
-    if (p + 1 < sp.P) {
+    if (p + 1 < L.P) {
       if (mode == 2 || mode == 4) {
         real xp[14], lam[2];
         wb_impact<real>(x, mode == 2 ? kFront : kBack, xp, lam);
         for (int i = 0; i < 14; ++i) x[i] = xp[i];
       }
-      if (p + 1 >= sp.n_wb) {
+      if (p + 1 >= L.n_wb) {
         const real t0 = x[0], t1 = x[1], t2 = x[2], t7 = x[7], t8 = x[8], t9 = x[9];
         x[0] = t0; x[1] = t1; x[2] = t2; x[3] = t7; x[4] = t8; x[5] = t9;
       }
@@ -1300,11 +1343,11 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   // (zero) controls and zero gains -- u = (0 + 0*0) + sum 0*(x - 0) = +0 exactly -- so the
   // nominal is completed here and forward_sweep(0) reduces to a cost evaluation (k_cost).
   // Both lanes run the (cheap) SRB chain; each writes half of every record.
-  if (sp.n_wb == 0)
+  if (L.n_wb == 0)
     for (int i = 0; i < 6; ++i) x[i] = x0[i];
-  for (int p = sp.n_wb; p < sp.P; ++p) {
-    const int mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
-    const real dt = sp.dt[p];
+  for (int p = L.n_wb; p < L.P; ++p) {
+    const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
+    const real dt = L.dt[p];
     real f[4], s[2];
     plan_foothold(x, dt * N, mode, f);
     srb_contact(mode, s);
@@ -1335,8 +1378,10 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
 // ============================================================================================
 __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_iter) {
   MHPC_NO_FMA_F32
-  const int b = blockIdx.x;
-  if (b >= sp.B) return;
+  const GrpBlk gb = block_group(sp, blockIdx.x, 1);  // one problem a block
+  if (gb.g < 0) return;
+  const Layout& L = layout_of(d, gb.g);
+  const int b = prob_at(sp, d, gb.p0);
   ProbState* st = &d.st[b];
   if (!st->active) return;
   const int lane = threadIdx.x;
@@ -1349,30 +1394,30 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   const bool reb = cap_reb && !reb_off;
   const int nom = st->nom_slot;
   const real* refpos = d.refpos + (size_t)b * sp.NK;
-  for (int kk = lane; kk < sp.NK; kk += 64) {
+  for (int kk = lane; kk < L.NK; kk += 64) {
     int p = 0;
-    while (p + 1 < sp.P && kk >= sp.ko[p + 1]) ++p;
-    const int k = kk - sp.ko[p], mode = sp.mode[p];
+    while (p + 1 < L.P && kk >= L.ko[p + 1]) ++p;
+    const int k = kk - L.ko[p], mode = L.mode[p];
     real c = real(0.0);
-    if (k < sp.N[p] - 1) {
+    if (k < L.N[p] - 1) {
       const real* r = traj_ptr(sp, d, b, nom, kk);
-      if (p < sp.n_wb)
-        c = wb_running_cost(sp, mode, sp.dt[p], refpos[kk], r, r + 14, r + 18, reb, st->delta[p],
+      if (p < L.n_wb)
+        c = wb_running_cost(sp, mode, L.dt[p], refpos[kk], r, r + 14, r + 18, reb, st->delta[p],
                             st->eps_tq[p], st->eps_grf[p]);
       else
-        c = fb_running_cost(sp, mode, sp.dt[p], refpos[kk], r, r + 6);
+        c = fb_running_cost(sp, mode, L.dt[p], refpos[kk], r, r + 6);
     }
     sc[kk] = c;
   }
   __syncthreads();
-  if (lane < sp.P) {
+  if (lane < L.P) {
     MHPC_NO_FMA_COST
-    const int p = lane, mode = sp.mode[p], N = sp.N[p], ko = sp.ko[p];
+    const int p = lane, mode = L.mode[p], N = L.N[p], ko = L.ko[p];
     acc V = 0;
     real h = 0;
     for (int k = 0; k < N - 1; ++k) V += sc[ko + k];
     const real* x = traj_ptr(sp, d, b, nom, ko + N - 1);
-    if (p < sp.n_wb) {
+    if (p < L.n_wb) {
       real rx[14];
       wb_term_ref(sp, mode, refpos[ko + N - 1], rx);
       acc Phi = 0;
@@ -1400,7 +1445,7 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
   __syncthreads();
   if (lane == 0) {
     acc J = 0, viol2 = 0;
-    for (int p = 0; p < sp.P; ++p) {
+    for (int p = 0; p < L.P; ++p) {
       J += sV[p];
       viol2 += acc(sH[p]) * sH[p];
       st->V[p] = sV[p];
@@ -1414,7 +1459,7 @@ __global__ __launch_bounds__(64) void k_cost(SolveParams sp, DevBufs d, int al_i
     st->par_slot = nom;  // forward_sweep(0) evaluated the partials (with AL, B1) here
     st->par_al = sp.AL_active ? 1 : 0;
     st->ls_nt = 0;
-    for (int p = 0; p < sp.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
+    for (int p = 0; p < L.P; ++p) { st->par_sigma[p] = st->sigma[p]; st->par_lambda[p] = st->lambda[p]; }
     st->al_iter = al_iter;
     st->reg = 0;
     st->ddp_active = 1;
@@ -1510,7 +1555,7 @@ __global__ void k_eval_srb(int n, const real* x, const real* u, const real* p,
   srb_jacobians(x + (size_t)i * 6, u + (size_t)i * 4, p + (size_t)i * 4, s + (size_t)i * 2, Ac + (size_t)i * 36, Bc + (size_t)i * 24);
 }
 
-// Sum the per-problem counters of the batch (int64 atomics into NCNT slots).
+// Sum the per-problem counters of each layout group (int64 atomics into NCNT slots per group).
 // One block of 256 threads, strided over the batch, tree-reduced in LDS: NCNT atomics per
 // block instead of per problem (the per-problem atomics on NCNT words serialised, ~35 us).
 __global__ __launch_bounds__(256) void k_reduce_counters(SolveParams sp, DevBufs d,
@@ -1520,9 +1565,12 @@ __global__ __launch_bounds__(256) void k_reduce_counters(SolveParams sp, DevBufs
   unsigned long long acc[NCNT];
 #pragma unroll
   for (int i = 0; i < NCNT; ++i) acc[i] = 0;
-  for (int b = blockIdx.x * 256 + t; b < sp.B; b += gridDim.x * 256)
+  const int g = blockIdx.y;  // layout group: its problems' totals go to out[g]
+  for (int pos = sp.go[g] + blockIdx.x * 256 + t; pos < sp.go[g + 1]; pos += gridDim.x * 256) {
+    const int b = prob_at(sp, d, pos);
 #pragma unroll
     for (int i = 0; i < NCNT; ++i) acc[i] += (unsigned long long)d.st[b].cnt[i];
+  }
 #pragma unroll
   for (int i = 0; i < NCNT; ++i) part[i][t] = acc[i];
   __syncthreads();
@@ -1532,45 +1580,60 @@ __global__ __launch_bounds__(256) void k_reduce_counters(SolveParams sp, DevBufs
       for (int i = 0; i < NCNT; ++i) part[i][t] += part[i][t + w];
     __syncthreads();
   }
-  if (t < NCNT) atomicAdd(&out[t], part[t][0]);
+  if (t < NCNT) atomicAdd(&out[g * NCNT + t], part[t][0]);
 }
 
 // ---- launchers (called by mhpc_runtime.cpp) ---------------------------------------------
+// Blocks of a launch over the layout groups with `per` problems a block (block_group)
+static unsigned grid_of(const SolveParams& sp, int per) {
+  long n = 0;
+  for (int g = 0; g < sp.ngrp; ++g) n += (sp.go[g + 1] - sp.go[g] + per - 1) / per;
+  return (unsigned)n;
+}
+// ... and with items[g] (or n_items) work items per problem, nt a block (block_group_items)
+static unsigned grid_items(const SolveParams& sp, const int* items, int n_items, int nt) {
+  long n = 0;
+  for (int g = 0; g < sp.ngrp; ++g)
+    n += ((long)(sp.go[g + 1] - sp.go[g]) * (items ? items[g] : n_items) + nt - 1) / nt;
+  return (unsigned)n;
+}
+// Problems of a launch (a sub-batch's share of the batch)
+int launch_problems(const SolveParams& sp) { return sp.go[sp.ngrp] - sp.go[0]; }
 hipError_t launch_reduce_counters(const SolveParams& sp, const DevBufs& d,
                                   unsigned long long* out, hipStream_t s) {
   const int nb = std::min((sp.B + 255) / 256, 64);
-  hipLaunchKernelGGL(k_reduce_counters, dim3(nb), dim3(256), 0, s, sp, d, out);
+  hipLaunchKernelGGL(k_reduce_counters, dim3(nb, sp.ngrp), dim3(256), 0, s, sp, d, out);
   return hipGetLastError();
 }
 hipError_t launch_reset(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3((2 * sp.B + 63) / 64), dim3(64), 0, s, sp, d, 0);
+  hipLaunchKernelGGL(k_init, dim3(grid_of(sp, 32)), dim3(64), 0, s, sp, d, 0);
   return hipGetLastError();
 }
 hipError_t launch_reset_arrays(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
   // ~64 elements per lane, at most 2 blocks per CU
-  const long e = (long)sp.B * sp.NK * 74 + (long)sp.B * sp.nslot * sp.P;
+  const long e = (long)sp.B * sp.NK * 74 + (long)sp.B * sp.nslot * sp.pmax;
   const long nb = std::min((e + 256 * 64 - 1) / (256 * 64), 2L * sp.ncu);
   hipLaunchKernelGGL(k_reset_arrays, dim3((unsigned)nb), dim3(256), 0, s, sp, d);
   return hipGetLastError();
 }
 hipError_t launch_init(const SolveParams& sp, const DevBufs& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3((2 * sp.B + 63) / 64), dim3(64), 0, s, sp, d, 1);
+  hipLaunchKernelGGL(k_init, dim3(grid_of(sp, 32)), dim3(64), 0, s, sp, d, 1);
   return hipGetLastError();
 }
 hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hipStream_t s) {
-  hipLaunchKernelGGL(k_cost, dim3(sp.B), dim3(64), 0, s, sp, d, al_iter);
+  hipLaunchKernelGGL(k_cost, dim3(grid_of(sp, 1)), dim3(64), 0, s, sp, d, al_iter);
   return hipGetLastError();
 }
 
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
                           int max_ddp, int full, hipStream_t s) {
   if (full) {
-    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
+    hipLaunchKernelGGL((k_rollout<false, false, false>), dim3(grid_of(sp, 64)), dim3(64), 0, s,
                        sp, d, al_iter, 0, 0, 1);
     return hipGetLastError();
   }
   const int ppw = 64 / sp.n_cand;
-  const int nblk = (sp.B + ppw - 1) / ppw;
+  const int nblk = (int)grid_of(sp, ppw);
   const int ncu = sp.ncu;
 #ifdef MHPC_RO_PIPE
   bool pipe = MHPC_RO_PIPE;
@@ -1579,12 +1642,11 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
                                 // wave per block only competes for issue slots
 #endif
   // staged: ST_PPW problems per wave at most, and every phase within the reference stage
-  bool fits = true;
-  for (int p = 0; p < sp.P; ++p) fits = fits && sp.N[p] <= ST_RMAX;
+  const bool fits = sp.stage_fits != 0;
   bool st = ppw <= ST_PPW && fits;
   // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
   const int ppw2 = std::min(32 / sp.n_cand, RO_PAIR_PPB);
-  const int nblk2 = ppw2 > 0 ? (sp.B + ppw2 - 1) / ppw2 : 0;
+  const int nblk2 = ppw2 > 0 ? (int)grid_of(sp, ppw2) : 0;
 #ifdef MHPC_RO_PAIR_MAX_BLK
   const int pair_max = MHPC_RO_PAIR_MAX_BLK;
 #else
@@ -1619,26 +1681,25 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
   // at once
   if (sp.ro_store < sp.n_cand - 1) {
     if (fits)
-      hipLaunchKernelGGL((k_rollout<false, true, false>), dim3((sp.B + ST_PPW - 1) / ST_PPW), dim3(64),
+      hipLaunchKernelGGL((k_rollout<false, true, false>), dim3(grid_of(sp, ST_PPW)), dim3(64),
                          0, s, sp, d, al_iter, 0, 0, 2);
     else
-      hipLaunchKernelGGL((k_rollout<false, false, false>), dim3((sp.B + 63) / 64), dim3(64), 0, s,
+      hipLaunchKernelGGL((k_rollout<false, false, false>), dim3(grid_of(sp, 64)), dim3(64), 0, s,
                          sp, d, al_iter, 0, 0, 2);
   }
   return hipGetLastError();
 }
 hipError_t launch_eps_rollout(const SolveParams& sp, const DevBufs& d, int n_eps,
                               const real* eps, real* J, real* viol, hipStream_t s) {
-  const long n = (long)sp.B * n_eps;
-  hipLaunchKernelGGL(k_eps_rollout, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, d, n_eps,
-                     eps, J, viol);
+  hipLaunchKernelGGL(k_eps_rollout, dim3(grid_items(sp, nullptr, n_eps, 64)), dim3(64), 0, s, sp, d,
+                     n_eps, eps, J, viol);
   return hipGetLastError();
 }
-hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real* lx,
-                            real* phix, hipStream_t s) {
-  const long n = (long)sp.B * sp.N[p];
-  hipLaunchKernelGGL(k_cost_grad, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d, p, lx,
-                     phix);
+hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int g, int p, int N, int b0,
+                            int nb, real* lx, real* phix, hipStream_t s) {
+  const long n = (long)nb * N;
+  hipLaunchKernelGGL(k_cost_grad, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, sp, d, g, p,
+                     b0, nb, lx, phix);
   return hipGetLastError();
 }
 // The direction groups write disjoint columns of the records: with a second stream s3 the
@@ -1648,7 +1709,7 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int p, real
 // joins s3 before returning.
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s, hipStream_t s3,
                            hipEvent_t fork, hipEvent_t join) {
-  const long tk = (long)sp.B * sp.par_knots, ti = (long)sp.B * sp.par_imp;
+  const unsigned tk = grid_items(sp, sp.gpk, 0, MHPC_PAR_BLOCK), ti = grid_items(sp, sp.gpi, 0, 256);
   const bool two = s3 && fork && join && kParGroups == 2 && tk > 0;
   if (two) {
     hipError_t e = hipEventRecord(fork, s);
@@ -1657,7 +1718,7 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   }
   if (tk > 0) {
     constexpr int nt = MHPC_PAR_BLOCK;
-    const dim3 grid((unsigned)((tk + nt - 1) / nt));
+    const dim3 grid(tk);
     hipLaunchKernelGGL(k_partials<1>, grid, dim3(nt), 0, two ? s3 : s, sp, d);
     hipLaunchKernelGGL(k_partials<0>, grid, dim3(nt), 0, s, sp, d);
     if (kParGroups == 4) {
@@ -1666,7 +1727,7 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
     }
   }
   if (ti > 0)
-    hipLaunchKernelGGL(k_partials_impact, dim3((unsigned)((ti + 255) / 256)), dim3(256), 0, two ? s3 : s,
+    hipLaunchKernelGGL(k_partials_impact, dim3(ti), dim3(256), 0, two ? s3 : s,
                        sp, d);
   if (two) {
     hipError_t e = hipEventRecord(join, s3);
@@ -1676,7 +1737,7 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   return hipGetLastError();
 }
 hipError_t launch_al_end(const SolveParams& sp, const DevBufs& d, int last, hipStream_t s) {
-  hipLaunchKernelGGL(k_al_end, dim3((sp.B + 63) / 64), dim3(64), 0, s, sp, d, last);
+  hipLaunchKernelGGL(k_al_end, dim3(grid_of(sp, 64)), dim3(64), 0, s, sp, d, last);
   return hipGetLastError();
 }
 hipError_t launch_export(const SolveParams& sp, const DevBufs& d, hipStream_t s) {

@@ -9,6 +9,8 @@
 #include <cmath>
 #include <string>
 #include <algorithm>
+#include <map>
+#include <numeric>
 #include <vector>
 
 #include "../../include/mhpc_capi.h"
@@ -25,11 +27,12 @@ bool bws_split(const SolveParams&);
 int ro_store_default();
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
-hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, hipStream_t);
+hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, int, hipStream_t);
 // N_TIMESTEPS_MAX (MHPCLocomotion.h): knots per phase buffer; record = x,u,y + K + du + G
 constexpr int kPhaseBufKnots = 110;
 constexpr int kStoreRec = KS + 56 + 4 + 14;
-hipError_t launch_cost_grad(const SolveParams&, const DevBufs&, int, real*, real*, hipStream_t);
+hipError_t launch_cost_grad(const SolveParams&, const DevBufs&, int, int, int, int, int, real*, real*,
+                            hipStream_t);
 hipError_t launch_eps_rollout(const SolveParams&, const DevBufs&, int, const real*, real*,
                               real*, hipStream_t);
 hipError_t launch_al_end(const SolveParams&, const DevBufs&, int, hipStream_t);
@@ -73,8 +76,20 @@ enum { K_INIT = 0, K_FULL, K_LS, K_PAR, K_BWS, K_AL, K_BWS_SRB, NKERN };
 static const char* kKernelNames[NKERN] = {"k_init", "k_cost(forward_sweep0)", "k_rollout(linesearch)",
                                           "k_partials", "k_bws", "k_al_end", "k_bws_srb"};
 
-struct Handle {
+// Per-problem phase layout: the descriptor (gait point) and the phase-buffer rotation of the
+// receding-horizon loop (MHPCLocomotion::update_problem rotates pidx_WB / pidx_FB by one per
+// call, MHPCLocomotion.cpp:111-121: after r calls phase i uses buffer (i + r) mod n).
+struct ProbLayout {
   mhpc_problem_desc desc;
+  int rot_wb, rot_fb;
+};
+// Algorithmic bytes per problem of one layout
+struct ByteModel {
+  double roll_read = 0, roll_write = 0, roll_term = 0, par = 0, init = 0, cost = 0;
+};
+
+struct Handle {
+  mhpc_problem_desc desc;  // the descriptor of mhpc_create (precision, vel, height)
   mhpc_hsddp_option opt;
   int device = 0;
   SolveParams sp;
@@ -91,23 +106,32 @@ struct Handle {
   // would mix new limits with old initial values -- refused until then
   bool params_changed = false;
   float solve_ms = 0;
-  unsigned long long* dcnt = nullptr;  // reduced counters of the batch [NCNT]
-  unsigned long long cnt[NCNT] = {};
+  unsigned long long* dcnt = nullptr;  // reduced counters per layout group [MAXL][NCNT]
+  unsigned long long cnt[NCNT] = {};   // their sum over the groups
+  unsigned long long gcnt[MAXL][NCNT] = {};
   // profiling: one event pair per launch of a solve, accumulated per kernel id
   bool profile = false;
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;
   double kms[NKERN] = {}, kbytes[NKERN] = {}, kflops[NKERN] = {};
   int64_t klaunch[NKERN] = {};
-  // algorithmic byte model per problem
-  double by_roll_read = 0, by_roll_write = 0, by_roll_term = 0, by_par = 0, by_init = 0, by_cost = 0;
-  // receding horizon (MHPCLocomotion::update_problem): current mode, phase-buffer rotation,
-  // buffer store, knot capacity of the packed arrays, and whether the next solve's first
-  // forward_sweep(0) must be a real rollout (rotated nominal, new x0)
-  int cmode = 1;
-  std::vector<int> pidx_wb, pidx_fb;
+  // per-problem layouts and the layout groups built from them (rebuild_groups): the layout
+  // table (host / device), each problem's layout, the problems grouped by layout
+  std::vector<ProbLayout> pl;
+  std::vector<Layout> lays;
+  std::vector<mhpc_problem_desc> ldesc;  // descriptor of each layout
+  std::vector<int> lid, gidx;
+  Layout* dlay = nullptr;
+  int *dgidx = nullptr, *dlid = nullptr;
+  // algorithmic byte model per problem of each layout
+  std::vector<ByteModel> bym;
+  // receding horizon (MHPCLocomotion::update_problem): each problem's current mode, the
+  // buffer store [B][spmax][nbk] (allocated at the first update), knot capacity of the
+  // packed arrays, and whether the next solve's first forward_sweep(0) must be a real
+  // rollout (rotated nominal, new x0)
+  std::vector<int> cmode;
   real* store = nullptr;
-  int nbk = 0, nk_cap = 0;
+  int nbk = 0, nk_cap = 0, spmax = 0;
   bool need_full = false;
   bool store_valid = false;  // store zeroed since the last initialize (memory_reset)
   // sub-batches (MHPC_VARIANT_SUBBATCH): the solve schedule runs once per contiguous block of
@@ -122,44 +146,47 @@ struct Handle {
   hipEvent_t evstart = nullptr;
 };
 
-// Phase layout of a descriptor: modes, knot counts and offsets, partials work items.
-static void layout_params(SolveParams& sp, const mhpc_problem_desc& desc) {
-  sp.P = desc.n_wb + desc.n_fb;
-  sp.n_wb = desc.n_wb;
+// Phase layout of a descriptor: modes, knot counts and offsets, partials work items, and the
+// phase buffers after rot_wb / rot_fb rotations (MHPCLocomotion::update_problem).
+static void build_layout(Layout& L, const mhpc_problem_desc& desc, int rot_wb, int rot_fb) {
+  memset(&L, 0, sizeof L);
+  L.P = desc.n_wb + desc.n_fb;
+  L.n_wb = desc.n_wb;
   int ko = 0, items = 0, items_v = 0;
-  for (int p = 0; p < sp.P; ++p) {
+  for (int p = 0; p < L.P; ++p) {
     const bool wb = p < desc.n_wb;
-    sp.mode[p] = desc.mode_seq[p];
-    sp.N[p] = desc.N[p];
-    sp.ko[p] = ko;
-    sp.xs[p] = wb ? 14 : 6;
-    sp.dt[p] = wb ? desc.dt_wb : desc.dt_fb;
+    L.mode[p] = desc.mode_seq[p];
+    L.N[p] = desc.N[p];
+    L.ko[p] = ko;
+    L.xs[p] = wb ? 14 : 6;
+    L.dt[p] = wb ? desc.dt_wb : desc.dt_fb;
+    L.buf[p] = wb ? (p + rot_wb) % desc.n_wb : desc.n_wb + (p - desc.n_wb + rot_fb) % desc.n_fb;
     ko += desc.N[p];
-    sp.par_knot_off[p] = items;
-    sp.par_imp_off[p] = items_v;
+    L.par_knot_off[p] = items;
+    L.par_imp_off[p] = items_v;
     if (wb) {
       items += desc.N[p] - 1;
-      items_v += (sp.mode[p] == 2 || sp.mode[p] == 4) ? 14 : 0;
+      items_v += (L.mode[p] == 2 || L.mode[p] == 4) ? 14 : 0;
     }
   }
-  for (int p = sp.P; p <= MAXP; ++p) {
-    sp.par_knot_off[p] = items;
-    sp.par_imp_off[p] = items_v;
+  for (int p = L.P; p <= MAXP; ++p) {
+    L.par_knot_off[p] = items;
+    L.par_imp_off[p] = items_v;
   }
-  sp.par_knots = items;
-  sp.par_imp = items_v;
-  sp.NK = ko;
+  L.par_knots = items;
+  L.par_imp = items_v;
+  L.NK = ko;
 }
 
 // Algorithmic HBM bytes (fp64) of one problem for each kernel's unit of work.
 constexpr double kB = sizeof(real);  // bytes per element of the solve's arithmetic type
 
-static void byte_model(Handle* h) {
-  const SolveParams& sp = h->sp;
-  double rr = 14 * 8, rw = 0, rt = 0, pb = 0, ib = sp.NK * kB, cb = 0;
-  for (int p = 0; p < sp.P; ++p) {
-    const bool wb = p < sp.n_wb;
-    const int n = wb ? 14 : 6, N = sp.N[p];
+static ByteModel byte_model(const Layout& L) {
+  ByteModel m;
+  double rr = 14 * 8, rw = 0, rt = 0, pb = 0, ib = L.NK * kB, cb = 0;
+  for (int p = 0; p < L.P; ++p) {
+    const bool wb = p < L.n_wb;
+    const int n = wb ? 14 : 6, N = L.N[p];
     // nominal x,u (n+4) + K (4n) + du (4) read once per problem (the candidates of a
     // problem share them)
     rr += (N - 1) * kB * ((n + 4) + 4 * n + 4);
@@ -171,18 +198,19 @@ static void byte_model(Handle* h) {
     // k_init: x,u,y written for every knot (WB and SRB)
     if (!wb) ib += N * kB * 14;
     if (wb) {
-      const bool imp = sp.mode[p] == 2 || sp.mode[p] == 4;
+      const bool imp = L.mode[p] == 2 || L.mode[p] == 4;
       // x,u read; the record written without its four zero columns (written once at create)
       pb += (N - 1) * kB * (18 + PS - 4 * 9) + (imp ? kB * (14 + 196) : 0.0);
       ib += N * kB * 22;
     }
   }
-  h->by_roll_read = rr;
-  h->by_roll_write = rw;
-  h->by_roll_term = rt;
-  h->by_par = pb;
-  h->by_init = ib;
-  h->by_cost = cb;
+  m.roll_read = rr;
+  m.roll_write = rw;
+  m.roll_term = rt;
+  m.par = pb;
+  m.init = ib;
+  m.cost = cb;
+  return m;
 }
 // backward sweep: per WB knot partials record + x,u,y + refpos read, K,du,G written;
 // per SRB knot x,u + refpos read, K,du,G written; Px read per impact-aware step
@@ -222,10 +250,134 @@ static int validate(const mhpc_problem_desc* d) {
 
 static void free_bufs(Handle* h) {
   DevBufs& d = h->d;
-  void* ptrs[] = {d.traj, d.refpos, d.K, d.du, d.G, d.par, d.px, d.x0, d.st, d.out, d.carry};
+  void* ptrs[] = {d.traj, d.refpos, d.K, d.du, d.G, d.par, d.px, d.x0, d.st, d.out, d.carry,
+                  h->dlay, h->dgidx, h->dlid};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   memset(&d, 0, sizeof d);
+  h->dlay = nullptr;
+  h->dgidx = h->dlid = nullptr;
+}
+
+// A descriptor normalised for comparison (entries past its phases and reserved fields zero)
+static mhpc_problem_desc norm_desc(const mhpc_problem_desc& in) {
+  mhpc_problem_desc d;
+  memset(&d, 0, sizeof d);
+  d.n_wb = in.n_wb;
+  d.n_fb = in.n_fb;
+  for (int p = 0; p < in.n_wb + in.n_fb; ++p) {
+    d.mode_seq[p] = in.mode_seq[p];
+    d.N[p] = in.N[p];
+  }
+  d.dt_wb = in.dt_wb;
+  d.dt_fb = in.dt_fb;
+  d.vel_cmd = in.vel_cmd;
+  d.height_cmd = in.height_cmd;
+  d.precision = in.precision;
+  return d;
+}
+
+// The packed per-knot arrays for a knot stride of NK (grown, never shrunk: their content is
+// rebuilt by initialize / update_problem; the partials records' zero columns are zeroed here
+// once, no kernel writes them).
+static int ensure_knot_arrays(Handle* h, int NK) {
+  if (NK <= h->nk_cap) return MHPC_OK;
+  DevBufs& d = h->d;
+  const size_t B = h->sp.B, nk = NK;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  real** arr[] = {&d.traj, &d.refpos, &d.K, &d.du, &d.G, &d.par, &d.out};
+  const size_t per[] = {(size_t)h->sp.nslot * KS, 1, 56, 4, 14, PS, KS};
+  for (int i = 0; i < 7; ++i) {
+    if (*arr[i]) HIPCHK(hipFree(*arr[i]));
+    *arr[i] = nullptr;
+    HIPCHK(hipMalloc((void**)arr[i], B * nk * per[i] * sizeof(real)));
+  }
+  HIPCHK(hipMemsetAsync(d.traj, 0, B * h->sp.nslot * nk * KS * sizeof(real), h->stream));
+  HIPCHK(hipMemsetAsync(d.par, 0, B * nk * PS * sizeof(real), h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->nk_cap = NK;
+  return MHPC_OK;
+}
+
+// Layout groups from the per-problem layouts: the distinct (descriptor, buffer rotation)
+// pairs, longest layout first (its blocks head every launch: the long blocks start first in a
+// mixed batch), the problems of each group in batch order.  Uploads the layout table and the
+// grouped order, sets the launch fields of sp, grows the packed arrays if a layout needs it.
+static int rebuild_groups(Handle* h) {
+  SolveParams& sp = h->sp;
+  const int B = sp.B;
+  std::map<std::string, int> seen;
+  std::vector<ProbLayout> uniq;
+  std::vector<int> first_lid(B);
+  for (int b = 0; b < B; ++b) {
+    ProbLayout k;
+    memset(&k, 0, sizeof k);
+    k.desc = norm_desc(h->pl[b].desc);
+    k.rot_wb = k.desc.n_wb > 0 ? h->pl[b].rot_wb % k.desc.n_wb : 0;
+    k.rot_fb = k.desc.n_fb > 0 ? h->pl[b].rot_fb % k.desc.n_fb : 0;
+    const std::string key((const char*)&k, sizeof k);
+    auto it = seen.find(key);
+    if (it == seen.end()) {
+      if ((int)uniq.size() == MAXL) return fail(MHPC_ERR_INVALID, "more than MHPC_MAX_LAYOUTS distinct layouts");
+      it = seen.emplace(key, (int)uniq.size()).first;
+      uniq.push_back(k);
+    }
+    first_lid[b] = it->second;
+  }
+  const int L = (int)uniq.size();
+  std::vector<Layout> lay(L);
+  for (int l = 0; l < L; ++l) build_layout(lay[l], uniq[l].desc, uniq[l].rot_wb, uniq[l].rot_fb);
+  std::vector<int> order(L), rank(L);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return lay[a].NK > lay[c].NK; });
+  for (int g = 0; g < L; ++g) rank[order[g]] = g;
+  h->lays.resize(L);
+  h->ldesc.resize(L);
+  h->bym.resize(L);
+  int NK = 0, pmax = 0;
+  sp.split_ok = 0;
+  sp.stage_fits = 1;
+  for (int g = 0; g < L; ++g) {
+    const Layout& Lg = lay[order[g]];
+    h->lays[g] = Lg;
+    h->ldesc[g] = uniq[order[g]].desc;
+    h->bym[g] = byte_model(Lg);
+    NK = std::max(NK, Lg.NK);
+    pmax = std::max(pmax, Lg.P);
+    if (Lg.n_wb > 0 && Lg.P > Lg.n_wb) sp.split_ok = 1;
+    for (int p = 0; p < Lg.P; ++p)
+      if (Lg.N[p] > ST_RMAX) sp.stage_fits = 0;
+    sp.gpk[g] = Lg.par_knots;
+    sp.gpi[g] = Lg.par_imp;
+  }
+  h->lid.resize(B);
+  std::vector<int> cnt(L + 1, 0);
+  for (int b = 0; b < B; ++b) {
+    h->lid[b] = rank[first_lid[b]];
+    ++cnt[h->lid[b] + 1];
+  }
+  sp.ngrp = L;
+  for (int g = 0; g < L; ++g) cnt[g + 1] += cnt[g];
+  for (int g = 0; g <= L; ++g) sp.go[g] = cnt[g];
+  h->gidx.resize(B);
+  sp.ident = 1;
+  for (int b = 0; b < B; ++b) {
+    const int pos = cnt[h->lid[b]]++;
+    h->gidx[pos] = b;
+    if (pos != b) sp.ident = 0;
+  }
+  sp.pmax = pmax;
+  int rc = ensure_knot_arrays(h, NK);
+  if (rc) return rc;
+  sp.NK = NK;
+  h->d.lay = h->dlay;
+  h->d.gidx = h->dgidx;
+  h->d.lid = h->dlid;
+  HIPCHK(hipMemcpyAsync(h->dlay, h->lays.data(), L * sizeof(Layout), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->dgidx, h->gidx.data(), B * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->dlid, h->lid.data(), B * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return MHPC_OK;
 }
 
 // Host (double) parameter structs <-> the kernels' parameter block (real).
@@ -339,18 +491,16 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   HIPCHK(hipSetDevice(device));
 
   Handle* h = new Handle();
-  h->desc = *desc;
+  h->desc = norm_desc(*desc);
   h->opt = *opt;
   h->device = device;
   SolveParams& sp = h->sp;
   memset(&sp, 0, sizeof sp);
   sp.B = batch;
-  layout_params(sp, *desc);
   // launch shapes follow this handle's device (one process may hold handles on several)
   if (hipDeviceGetAttribute(&sp.ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       sp.ncu < 1)
     sp.ncu = 256;
-  for (int p = 0; p < sp.P; ++p) sp.buf[p] = p;
   sp.vel = desc->vel_cmd;
   sp.height = desc->height_cmd;
   // line-search grid exactly as MultiPhaseDDP::forward_iteration generates it (:130-151)
@@ -383,30 +533,24 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
     put_weights(sp.cw, w);
     put_constraints(sp.cw, c);
   }
+  h->pl.assign(batch, ProbLayout{h->desc, 0, 0});
+  h->cmode.assign(batch, desc->mode_seq[0]);
 
   DevBufs& d = h->d;
   memset(&d, 0, sizeof d);
-  const size_t B = batch, NK = sp.NK;
+  const size_t B = batch;
   hipError_t e = hipSuccess;
   auto alloc = [&](void** p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, bytes);
   };
-  alloc((void**)&d.traj, B * sp.nslot * NK * KS * sizeof(real));
-  alloc((void**)&d.refpos, B * NK * sizeof(real));
-  alloc((void**)&d.K, B * NK * 56 * sizeof(real));
-  alloc((void**)&d.du, B * NK * 4 * sizeof(real));
-  alloc((void**)&d.G, B * NK * 14 * sizeof(real));
-  alloc((void**)&d.par, B * NK * PS * sizeof(real));
   alloc((void**)&d.px, B * MAXP * 196 * sizeof(real));
   alloc((void**)&d.x0, B * 14 * sizeof(real));
   alloc((void**)&d.st, B * sizeof(ProbState));
-  alloc((void**)&d.out, B * NK * KS * sizeof(real));
   alloc((void**)&d.carry, B * sizeof(BwsCarry));
-  alloc((void**)&h->dcnt, NCNT * sizeof(unsigned long long));
-  h->nk_cap = sp.NK;
-  h->nbk = kPhaseBufKnots;
-  for (int p = 0; p < sp.P; ++p) h->nbk = std::max(h->nbk, sp.N[p]);
-  alloc((void**)&h->store, B * sp.P * (size_t)h->nbk * kStoreRec * sizeof(real));
+  alloc((void**)&h->dcnt, MAXL * NCNT * sizeof(unsigned long long));
+  alloc((void**)&h->dlay, MAXL * sizeof(Layout));
+  alloc((void**)&h->dgidx, B * sizeof(int));
+  alloc((void**)&h->dlid, B * sizeof(int));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evfork, hipEventDisableTiming);
@@ -419,28 +563,34 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   // zero x0 on the handle's own (non-blocking) stream: a null-stream memset would not be
   // ordered before mhpc_set_x0's copy on this stream
   if (e == hipSuccess) e = hipMemsetAsync(d.x0, 0, B * 14 * sizeof(real), h->stream);
-  // the zero Jacobian columns of the partials records are never written by a kernel
-  if (e == hipSuccess) e = hipMemsetAsync(d.par, 0, B * NK * PS * sizeof(real), h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  byte_model(h);
-  if (e != hipSuccess) {
-    if (h->dcnt) (void)hipFree(h->dcnt);
-    if (h->store) (void)hipFree(h->store);
-    free_bufs(h);
-    delete h;
-    return fail(MHPC_ERR_DEVICE, std::string("allocation failed: ") + hipGetErrorString(e));
+  int rc2 = e == hipSuccess ? MHPC_OK : fail(MHPC_ERR_DEVICE, std::string("allocation failed: ") + hipGetErrorString(e));
+  if (!rc2) rc2 = rebuild_groups(h);  // one layout group; allocates the packed arrays
+  if (rc2) {
+    api_destroy(h);
+    return rc2;
   }
   *out = h;
   return MHPC_OK;
 }
 
+static int x0_row(const Handle* h) {
+  for (const Layout& L : h->lays)
+    if (L.n_wb > 0) return 14;
+  return 6;
+}
+
 int api_set_x0(Handle* h, const double* x0) {
   if (!h || !x0) return fail(MHPC_ERR_INVALID, "null argument");
   HIPCHK(hipSetDevice(h->device));
-  const int n0 = h->sp.n_wb > 0 ? 14 : 6;
+  // rows of 14 when any layout starts with a whole-body phase (an SRB-only problem reads the
+  // first 6 entries of its row), else 6
+  const int n0 = x0_row(h);
   std::vector<real> pad((size_t)h->sp.B * 14, real(0));
-  for (int b = 0; b < h->sp.B; ++b)
-    for (int i = 0; i < n0; ++i) pad[(size_t)b * 14 + i] = (real)x0[(size_t)b * n0 + i];
+  for (int b = 0; b < h->sp.B; ++b) {
+    const int nb = h->lays[h->lid[b]].n_wb > 0 ? 14 : 6;
+    for (int i = 0; i < nb; ++i) pad[(size_t)b * 14 + i] = (real)x0[(size_t)b * n0 + i];
+  }
   HIPCHK(hipMemcpyAsync(h->d.x0, pad.data(), pad.size() * sizeof(real), hipMemcpyHostToDevice,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -496,6 +646,18 @@ static int d2h(Handle* h, void* dst, const void* src, size_t bytes) {
 
 // initialization(): memory_reset + build_problem (refs) + warmstart, all on the device.
 static int initialize_async(Handle* h) {
+  // build_problem binds phase p to buffer p and starts the gait at each problem's first mode
+  bool rotated = false;
+  for (int b = 0; b < h->sp.B; ++b) {
+    ProbLayout& q = h->pl[b];
+    rotated = rotated || q.rot_wb != 0 || q.rot_fb != 0;
+    q.rot_wb = q.rot_fb = 0;
+    h->cmode[b] = q.desc.mode_seq[0];
+  }
+  if (rotated) {
+    const int rc = rebuild_groups(h);
+    if (rc) return rc;
+  }
   const SolveParams& sp = h->sp;
   DevBufs& d = h->d;
   // memory_reset (K / du / G, trajectory tails) on the second stream beside k_init, which
@@ -506,15 +668,9 @@ static int initialize_async(Handle* h) {
   HIPCHK(hipEventRecord(h->evjoin, h->stream2));
   LAUNCH(h, K_INIT, launch_init(sp, d, h->stream));
   HIPCHK(hipStreamWaitEvent(h->stream, h->evjoin, 0));
-  h->kbytes[K_INIT] += h->by_init * sp.B;
-  // build_problem binds phase p to buffer p; the buffer store is zeroed lazily (first
-  // update_problem), so a plain initialize + solve pays nothing for it
-  h->pidx_wb.clear();
-  h->pidx_fb.clear();
-  for (int i = 0; i < h->desc.n_wb; ++i) h->pidx_wb.push_back(i);
-  for (int i = 0; i < h->desc.n_fb; ++i) h->pidx_fb.push_back(i);
-  for (int p = 0; p < h->sp.P; ++p) h->sp.buf[p] = p;
-  h->cmode = h->desc.mode_seq[0];
+  for (int g = 0; g < sp.ngrp; ++g) h->kbytes[K_INIT] += h->bym[g].init * (sp.go[g + 1] - sp.go[g]);
+  // the buffer store is zeroed lazily (first update_problem), so a plain initialize + solve
+  // pays nothing for it
   h->store_valid = false;
   h->need_full = false;
   return MHPC_OK;
@@ -560,7 +716,7 @@ struct SolveBlock {
 };
 
 // Problems [b0, b0 + sp.B) of the handle's arrays as the kernels index them (b * per-problem
-// stride, with sp.NK the knot stride of the packed arrays).
+// stride, with sp.NK the knot stride of the packed arrays): for the layout-free export kernel.
 static DevBufs block_bufs(const DevBufs& d, const SolveParams& sp, size_t b0) {
   DevBufs o = d;
   const size_t NK = sp.NK;
@@ -692,9 +848,11 @@ static int solve_async(Handle* h) {
       const Handle::SubStreams& ss = h->subs[s];
       SolveBlock& k = blk[s];
       const int b0 = (int)((int64_t)s * B / nsub), b1 = (int)((int64_t)(s + 1) * B / nsub);
+      // the block's problems: gidx positions [b0, b1) (each group's range clipped to them);
+      // the arrays stay the handle's (gidx holds absolute problem indices)
       k.sp = h->sp;
-      k.sp.B = b1 - b0;
-      k.d = block_bufs(h->d, h->sp, (size_t)b0);
+      for (int g = 0; g <= k.sp.ngrp; ++g) k.sp.go[g] = std::min(std::max(h->sp.go[g], b0), b1);
+      k.d = h->d;
       k.s1 = ss.s1;
       k.s2 = ss.s2;
       k.fork = ss.fork;
@@ -738,8 +896,8 @@ static int solve_async(Handle* h) {
     if (rc) return rc;
     HIPCHK(ej);
   }
-  // batch totals of the per-problem counters (tiny reduction, NCNT words back)
-  HIPCHK(hipMemsetAsync(h->dcnt, 0, NCNT * sizeof(unsigned long long), h->stream));
+  // totals of the per-problem counters per layout group (tiny reduction, NCNT words each)
+  HIPCHK(hipMemsetAsync(h->dcnt, 0, (size_t)h->sp.ngrp * NCNT * sizeof(unsigned long long), h->stream));
   HIPCHK(launch_reduce_counters(h->sp, h->d, h->dcnt, h->stream));
   return MHPC_OK;
 }
@@ -758,24 +916,31 @@ int api_solve(Handle* h, int32_t* status) {
   int rc = solve_async(h);
   if (rc) return rc;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
-  HIPCHK(hipMemcpyAsync(h->cnt, h->dcnt, NCNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                        h->stream));
+  HIPCHK(hipMemcpyAsync(h->gcnt, h->dcnt, (size_t)h->sp.ngrp * NCNT * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  for (int i = 0; i < NCNT; ++i) {
+    h->cnt[i] = 0;
+    for (int g = 0; g < h->sp.ngrp; ++g) h->cnt[i] += h->gcnt[g][i];
+  }
   HIPCHK(hipEventElapsedTime(&h->solve_ms, h->ev0, h->ev1));
   h->solved = true;
   h->need_full = false;
   rc = collect_profile(h);
   if (rc) return rc;
   const unsigned long long* c = h->cnt;
-  h->kbytes[K_FULL] += c[C_FWD] * h->by_cost;
-  {  // the trials that store their records (RO_STORE_FIRST; the re-rolls of the others,
-     // rare, are not counted)
+  for (int g = 0; g < h->sp.ngrp; ++g) {  // per layout group: its problems' counters x its bytes
+    const unsigned long long* cg = h->gcnt[g];
+    const ByteModel& m = h->bym[g];
     const SolveParams& sp = h->sp;
+    h->kbytes[K_FULL] += cg[C_FWD] * m.cost;
+    // the trials that store their records (RO_STORE_FIRST; the re-rolls of the others, rare,
+    // are not counted)
     const double stored = std::min(sp.n_cand, sp.ro_store + 1);
-    h->kbytes[K_LS] += c[C_LS_LAUNCH] * h->by_roll_read +
-                       c[C_LS_RUN] * (h->by_roll_write * stored / sp.n_cand + h->by_roll_term);
+    h->kbytes[K_LS] += cg[C_LS_LAUNCH] * m.roll_read +
+                       cg[C_LS_RUN] * (m.roll_write * stored / sp.n_cand + m.roll_term);
+    h->kbytes[K_PAR] += cg[C_PAR_RUN] * m.par;
   }
-  h->kbytes[K_PAR] += c[C_PAR_RUN] * h->by_par;
   // the SRB half of a split sweep: the SRB knots of every first attempt; the rest (WB knots,
   // impact steps, SRB knots of retries) is the WB half's / the whole sweep's
   const unsigned long long fb1 = c[C_BWS_KNOTS_FB1], fb = c[C_BWS_KNOTS_FB] - fb1;
@@ -803,25 +968,19 @@ static int copy_rows(Handle* h, const real* src, int per, int ko, int N, size_t 
   return MHPC_OK;
 }
 
-// Problems [first, first + count) of one phase (count = batch: mhpc_get_phase).
-int api_get_phase(Handle* h, int phase, int first, int count, double* x, double* u, double* y,
-                  double* K, double* du, double* Vx) {
-  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
-  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+// Problems [first, first + count) of one phase (count = batch: mhpc_get_phase).  The range's
+// phase must have one shape (knots, state size); runs of problems whose phase starts at the
+// same knot offset are copied with one strided copy each.
+static int get_phase_run(Handle* h, int phase, int n, int N, int ko, size_t b0, size_t B, double* x,
+                         double* u, double* y, double* K, double* du, double* Vx) {
   const SolveParams& sp = h->sp;
-  if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
-  if (first < 0 || count < 1 || first > sp.B - count)
-    return fail(MHPC_ERR_INVALID, "problem range outside the batch");
-  HIPCHK(hipSetDevice(h->device));
-  const size_t B = count, b0 = first;
-  const int n = sp.xs[phase], N = sp.N[phase], ko = sp.ko[phase];
   std::vector<real> buf;
   int rc;
   if (x || u || y) {
     // export only the requested problems (a caller looping over problems would otherwise
-    // export the whole batch per call): the block's arrays as the solve's sub-batches see them
+    // export the whole batch per call)
     SolveParams sub = sp;
-    sub.B = count;
+    sub.B = (int)B;
     HIPCHK(launch_export(sub, block_bufs(h->d, sp, b0), h->stream));
     if ((rc = copy_rows(h, h->d.out, KS, ko, N, b0, B, buf))) return rc;
     for (size_t b = 0; b < B; ++b)
@@ -854,6 +1013,45 @@ int api_get_phase(Handle* h, int phase, int first, int count, double* x, double*
   return MHPC_OK;
 }
 
+// Shape check of a phase over a problem range: *n, *N of the phase (one shape for the range)
+static int range_phase_shape(const Handle* h, int phase, int first, int count, int* n, int* N) {
+  if (first < 0 || count < 1 || first > h->sp.B - count)
+    return fail(MHPC_ERR_INVALID, "problem range outside the batch");
+  for (int b = first; b < first + count; ++b) {
+    const Layout& L = h->lays[h->lid[b]];
+    if (phase < 0 || phase >= L.P) return fail(MHPC_ERR_INVALID, "bad phase");
+    if (b == first) {
+      *n = L.xs[phase];
+      *N = L.N[phase];
+    } else if (L.xs[phase] != *n || L.N[phase] != *N) {
+      return fail(MHPC_ERR_INVALID, "the phase differs in shape across the problem range (per-problem layouts)");
+    }
+  }
+  return MHPC_OK;
+}
+
+int api_get_phase(Handle* h, int phase, int first, int count, double* x, double* u, double* y,
+                  double* K, double* du, double* Vx) {
+  if (!h) return fail(MHPC_ERR_INVALID, "null handle");
+  if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
+  int n = 0, N = 0;
+  int rc = range_phase_shape(h, phase, first, count, &n, &N);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(h->device));
+  for (int r0 = first; r0 < first + count;) {
+    const int ko = h->lays[h->lid[r0]].ko[phase];
+    int r1 = r0 + 1;
+    while (r1 < first + count && h->lays[h->lid[r1]].ko[phase] == ko) ++r1;
+    const size_t o = (size_t)(r0 - first) * N;
+    auto at = [&](double* p, int per) { return p ? p + o * per : nullptr; };
+    rc = get_phase_run(h, phase, n, N, ko, r0, r1 - r0, at(x, n), at(u, 4), at(y, 4), at(K, 4 * n),
+                       at(du, 4), at(Vx, n));
+    if (rc) return rc;
+    r0 = r1;
+  }
+  return MHPC_OK;
+}
+
 int api_get_scalars(Handle* h, double* J, double* dV_exp, double* viol,
                                 double* V_phase, double* dV_phase, int32_t* trace) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
@@ -866,9 +1064,11 @@ int api_get_scalars(Handle* h, double* J, double* dV_exp, double* viol,
     if (J) J[b] = st[b].J;
     if (dV_exp) dV_exp[b] = st[b].dV_exp;
     if (viol) viol[b] = st[b].viol;
-    for (int p = 0; p < sp.P; ++p) {
-      if (V_phase) V_phase[b * sp.P + p] = st[b].V[p];
-      if (dV_phase) dV_phase[b * sp.P + p] = st[b].dV[p];
+    // rows of the most phases any layout has; zero past the problem's own phases
+    const int P = h->lays[h->lid[b]].P;
+    for (int p = 0; p < sp.pmax; ++p) {
+      if (V_phase) V_phase[b * sp.pmax + p] = p < P ? (double)st[b].V[p] : 0.0;
+      if (dV_phase) dV_phase[b * sp.pmax + p] = p < P ? (double)st[b].dV[p] : 0.0;
     }
     if (trace) memcpy(&trace[(size_t)b * TRACE], st[b].trace, TRACE * sizeof(int32_t));
   }
@@ -912,19 +1112,29 @@ int api_rollout_costs(Handle* h, int n_eps, const double* eps, double* J,
   return MHPC_OK;
 }
 
-int api_get_cost_gradients(Handle* h, int phase, double* lx, double* Phix) {
+int api_get_cost_gradients(Handle* h, int phase, int first, int count, double* lx, double* Phix) {
   if (!h) return fail(MHPC_ERR_INVALID, "null handle");
   if (!h->initialized) return fail(MHPC_ERR_STATE, "not initialized");
   const SolveParams& sp = h->sp;
-  if (phase < 0 || phase >= sp.P) return fail(MHPC_ERR_INVALID, "bad phase");
+  int n = 0, N = 0;
+  int rc = range_phase_shape(h, phase, first, count, &n, &N);
+  if (rc) return rc;
   HIPCHK(hipSetDevice(h->device));
-  const int n = phase < sp.n_wb ? 14 : 6, N = sp.N[phase];
-  const size_t nlx = (size_t)sp.B * (N - 1) * n, nph = (size_t)sp.B * n;
+  const size_t nlx = (size_t)count * (N - 1) * n, nph = (size_t)count * n;
   real *dlx = nullptr, *dph = nullptr;
   std::vector<real> hlx(nlx), hph(nph);
-  hipError_t e = hipMalloc((void**)&dlx, nlx * sizeof(real));
+  hipError_t e = hipMalloc((void**)&dlx, nlx * sizeof(real) + 8);
   if (e == hipSuccess) e = hipMalloc((void**)&dph, nph * sizeof(real));
-  if (e == hipSuccess) e = launch_cost_grad(sp, h->d, phase, dlx, dph, h->stream);
+  // one launch per run of problems with the same layout
+  for (int r0 = first; r0 < first + count && e == hipSuccess;) {
+    const int g = h->lid[r0];
+    int r1 = r0 + 1;
+    while (r1 < first + count && h->lid[r1] == g) ++r1;
+    const size_t o = (size_t)(r0 - first);
+    e = launch_cost_grad(sp, h->d, g, phase, N, r0, r1 - r0, dlx + o * (N - 1) * n, dph + o * n,
+                         h->stream);
+    r0 = r1;
+  }
   if (e == hipSuccess) e = hipMemcpyAsync(hlx.data(), dlx, nlx * sizeof(real), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(hph.data(), dph, nph * sizeof(real), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -938,74 +1148,100 @@ int api_get_cost_gradients(Handle* h, int phase, double* lx, double* Phix) {
   return MHPC_OK;
 }
 
-// MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158) for the whole batch: advance
-// the gait by one mode, rotate the WB and SRB phase buffers by one, recompute mode sequence
-// and knot counts, regenerate the references from the current x0 (mhpc_set_x0) and
-// re-initialise the AL / ReB parameters; the rotated nominal trajectories and gains are the
-// warm start of the next mhpc_solve, whose first forward_sweep(0) is then a real rollout.
-int api_update_problem(Handle* h, const mhpc_gait* gait) {
-  if (!h || !gait) return fail(MHPC_ERR_INVALID, "null argument");
+// The phase-buffer store of the receding-horizon loop, [B][spmax][nbk][SREC], zeroed at its
+// first use after an initialize (the reference's memory_reset of its phase buffers); sized for
+// the current layouts (buffers of N_TIMESTEPS_MAX = 110 knots, or the longest phase).
+static int ensure_store(Handle* h) {
+  if (h->store_valid) return MHPC_OK;
+  int nbk = kPhaseBufKnots;
+  for (const Layout& L : h->lays)
+    for (int p = 0; p < L.P; ++p) nbk = std::max(nbk, L.N[p]);
+  const int spmax = h->sp.pmax;
+  const size_t bytes = (size_t)h->sp.B * spmax * nbk * kStoreRec * sizeof(real);
+  if (!h->store || nbk != h->nbk || spmax != h->spmax) {
+    if (h->store) HIPCHK(hipFree(h->store));
+    h->store = nullptr;
+    HIPCHK(hipMalloc((void**)&h->store, bytes));
+    h->nbk = nbk;
+    h->spmax = spmax;
+  }
+  HIPCHK(hipMemsetAsync(h->store, 0, bytes, h->stream));
+  h->store_valid = true;
+  return MHPC_OK;
+}
+
+// MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158) per problem: problem b takes
+// steps[b] gait steps (each: rotate the WB and SRB phase buffers by one, advance the gait by
+// one mode, recompute mode sequence and knot counts -- Gait.h:48-77); then every problem's
+// references are regenerated from the current x0 (mhpc_set_x0) and its AL / ReB parameters
+// re-initialised.  The rotated nominal trajectories and gains are the warm start of the next
+// mhpc_solve, whose first forward_sweep(0) is then a real rollout.  Problems whose layouts
+// change move to the layout group of their new layout.
+int api_update_problems(Handle* h, int n_gaits, const mhpc_gait* gaits, const int32_t* gait_of,
+                        const int32_t* steps) {
+  if (!h || !gaits) return fail(MHPC_ERR_INVALID, "null argument");
   if (!h->initialized) return fail(MHPC_ERR_STATE, "mhpc_initialize must precede mhpc_update_problem");
-  if (gait->n_modes < 1 || gait->n_modes > MHPC_MAX_PHASES)
-    return fail(MHPC_ERR_INVALID, "gait needs 1..16 modes");
-  for (int i = 0; i < gait->n_modes; ++i)
-    if (gait->modes[i] < 1 || gait->modes[i] > 4) return fail(MHPC_ERR_INVALID, "gait mode out of range");
+  if (n_gaits < 1 || n_gaits > MAXL) return fail(MHPC_ERR_INVALID, "n_gaits must be 1..MHPC_MAX_LAYOUTS");
+  for (int gi = 0; gi < n_gaits; ++gi) {
+    const mhpc_gait& g = gaits[gi];
+    if (g.n_modes < 1 || g.n_modes > MHPC_MAX_PHASES)
+      return fail(MHPC_ERR_INVALID, "gait needs 1..16 modes");
+    for (int i = 0; i < g.n_modes; ++i)
+      if (g.modes[i] < 1 || g.modes[i] > 4) return fail(MHPC_ERR_INVALID, "gait mode out of range");
+  }
   HIPCHK(hipSetDevice(h->device));
-  // Gait::get_next_mode / get_mode_seq / get_timings (Gait.h:48-77)
-  auto next_mode = [&](int m) {
-    for (int i = 0; i < gait->n_modes; ++i)
-      if (gait->modes[i] == m) return gait->modes[(i + 1) % gait->n_modes];
-    return -1;  // the reference falls off the end of a non-void function here
-  };
-  const int cm = next_mode(h->cmode);
-  if (cm < 0) return fail(MHPC_ERR_INVALID, "current mode is not in the gait");
-  mhpc_problem_desc nd = h->desc;
-  const int P = h->sp.P;
-  nd.mode_seq[0] = cm;
-  for (int p = 1; p < P; ++p) nd.mode_seq[p] = next_mode(nd.mode_seq[p - 1]);
-  for (int p = 0; p < P; ++p) {
-    const float tm = gait->timings[nd.mode_seq[p] - 1];
-    const double dt = p < nd.n_wb ? nd.dt_wb : nd.dt_fb;
-    nd.N[p] = (int)std::round((double)tm / dt);  // round(float timing / (double) dt)
-    if (nd.N[p] < 2) return fail(MHPC_ERR_INVALID, "gait timing gives a phase with N < 2");
-    if (nd.N[p] > h->nbk) return fail(MHPC_ERR_INVALID, "phase longer than the phase buffers");
-  }
-  if (!h->store_valid) {  // memory_reset of the buffers (lazy, see initialize_async)
-    HIPCHK(hipMemsetAsync(h->store, 0, (size_t)h->sp.B * P * h->nbk * kStoreRec * sizeof(real),
-                          h->stream));
-    h->store_valid = true;
-  }
-  // phases write through to their buffers in the reference: save the current layout
-  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, 1, h->stream));
-  // rotate the buffer lists (front -> back) and bind the new phases
-  if (!h->pidx_wb.empty()) std::rotate(h->pidx_wb.begin(), h->pidx_wb.begin() + 1, h->pidx_wb.end());
-  if (!h->pidx_fb.empty()) std::rotate(h->pidx_fb.begin(), h->pidx_fb.begin() + 1, h->pidx_fb.end());
-  SolveParams sp = h->sp;
-  layout_params(sp, nd);
-  for (int p = 0; p < P; ++p)
-    sp.buf[p] = p < nd.n_wb ? h->pidx_wb[p] : nd.n_wb + h->pidx_fb[p - nd.n_wb];
-  if (sp.NK > h->nk_cap) {  // grow the packed arrays (their content comes from the store)
-    HIPCHK(hipStreamSynchronize(h->stream));
-    DevBufs& d = h->d;
-    const size_t B = sp.B, NK = sp.NK;
-    real** arr[] = {&d.traj, &d.refpos, &d.K, &d.du, &d.G, &d.par, &d.out};
-    const size_t per[] = {(size_t)sp.nslot * KS, 1, 56, 4, 14, PS, KS};
-    for (int i = 0; i < 7; ++i) {
-      HIPCHK(hipFree(*arr[i]));
-      *arr[i] = nullptr;
-      HIPCHK(hipMalloc((void**)arr[i], B * NK * per[i] * sizeof(real)));
+  int rc = ensure_store(h);
+  if (rc) return rc;
+  const int B = h->sp.B;
+  std::vector<ProbLayout> npl = h->pl;
+  std::vector<int> ncm = h->cmode;
+  for (int b = 0; b < B; ++b) {
+    const int gi = gait_of ? gait_of[b] : 0;
+    if (gi < 0 || gi >= n_gaits) return fail(MHPC_ERR_INVALID, "gait index out of range");
+    const int ns = steps ? steps[b] : 1;
+    if (ns < 0 || ns > 1024) return fail(MHPC_ERR_INVALID, "steps must be 0..1024");
+    const mhpc_gait& gait = gaits[gi];
+    // Gait::get_next_mode / get_mode_seq / get_timings (Gait.h:48-77)
+    auto next_mode = [&](int m) {
+      for (int i = 0; i < gait.n_modes; ++i)
+        if (gait.modes[i] == m) return gait.modes[(i + 1) % gait.n_modes];
+      return -1;  // the reference falls off the end of a non-void function here
+    };
+    mhpc_problem_desc& nd = npl[b].desc;
+    const int P = nd.n_wb + nd.n_fb;
+    for (int step = 0; step < ns; ++step) {
+      const int cm = next_mode(ncm[b]);
+      if (cm < 0) return fail(MHPC_ERR_INVALID, "current mode is not in the gait");
+      ncm[b] = cm;
+      nd.mode_seq[0] = cm;
+      for (int p = 1; p < P; ++p) nd.mode_seq[p] = next_mode(nd.mode_seq[p - 1]);
+      int NK = 0;
+      for (int p = 0; p < P; ++p) {
+        const float tm = gait.timings[nd.mode_seq[p] - 1];
+        const double dt = p < nd.n_wb ? nd.dt_wb : nd.dt_fb;
+        nd.N[p] = (int)std::round((double)tm / dt);  // round(float timing / (double) dt)
+        if (nd.N[p] < 2) return fail(MHPC_ERR_INVALID, "gait timing gives a phase with N < 2");
+        if (nd.N[p] > h->nbk) return fail(MHPC_ERR_INVALID, "phase longer than the phase buffers");
+        NK += nd.N[p];
+      }
+      if (NK > MHPC_MAX_KNOTS) return fail(MHPC_ERR_INVALID, "too many knots");
+      npl[b].rot_wb += 1;  // pidx_WB / pidx_FB: front -> back (MHPCLocomotion.cpp:111-121)
+      npl[b].rot_fb += 1;
     }
-    HIPCHK(hipMemsetAsync(d.traj, 0, B * sp.nslot * NK * KS * sizeof(real), h->stream));
-    HIPCHK(hipMemsetAsync(d.par, 0, B * NK * PS * sizeof(real), h->stream));
-    h->nk_cap = sp.NK;
   }
-  h->sp = sp;
-  h->desc = nd;
-  h->cmode = cm;
+  // phases write through to their buffers in the reference: save the current layouts
+  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, h->spmax, 1, h->stream));
+  const std::vector<ProbLayout> opl = h->pl;
+  h->pl = npl;
+  if ((rc = rebuild_groups(h))) {  // too many distinct layouts: keep the old ones
+    h->pl = opl;
+    (void)rebuild_groups(h);
+    return rc;
+  }
+  h->cmode = ncm;
   HIPCHK(launch_reset(h->sp, h->d, h->stream));  // refs from x0, AL/ReB init, nom_slot = 0
-  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, 0, h->stream));
+  HIPCHK(launch_store(h->sp, h->d, h->store, h->nbk, h->spmax, 0, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  byte_model(h);
   h->need_full = true;
   h->solved = false;
   h->x0_changed = false;
@@ -1013,11 +1249,65 @@ int api_update_problem(Handle* h, const mhpc_gait* gait) {
   return MHPC_OK;
 }
 
+int api_update_problem(Handle* h, const mhpc_gait* gait) {
+  return api_update_problems(h, 1, gait, nullptr, nullptr);
+}
+
+// Per-problem phase layouts (the batch axis over gait schedules): problem b gets
+// descs[lop[b]] with identity phase buffers; the handle is uninitialised afterwards.
+int api_set_layouts(Handle* h, int n_desc, const mhpc_problem_desc* descs, const int32_t* lop) {
+  if (!h || !descs) return fail(MHPC_ERR_INVALID, "null argument");
+  if (n_desc < 1 || n_desc > MAXL) return fail(MHPC_ERR_INVALID, "n_desc must be 1..MHPC_MAX_LAYOUTS");
+  for (int i = 0; i < n_desc; ++i) {
+    int rc = validate(&descs[i]);
+    if (rc) return rc;
+    if (descs[i].precision != h->desc.precision)
+      return fail(MHPC_ERR_INVALID, "a layout's precision differs from the handle's");
+    if (descs[i].vel_cmd != h->desc.vel_cmd || descs[i].height_cmd != h->desc.height_cmd)
+      return fail(MHPC_ERR_INVALID, "a layout's vel_cmd / height_cmd differs from the handle's");
+  }
+  const int B = h->sp.B;
+  for (int b = 0; lop && b < B; ++b)
+    if (lop[b] < 0 || lop[b] >= n_desc) return fail(MHPC_ERR_INVALID, "layout index out of range");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const std::vector<ProbLayout> opl = h->pl;
+  for (int b = 0; b < B; ++b) {
+    const mhpc_problem_desc& d = descs[lop ? lop[b] : b % n_desc];
+    h->pl[b] = ProbLayout{norm_desc(d), 0, 0};
+  }
+  int rc = rebuild_groups(h);
+  if (rc) {
+    h->pl = opl;
+    (void)rebuild_groups(h);
+    return rc;
+  }
+  for (int b = 0; b < B; ++b) h->cmode[b] = h->pl[b].desc.mode_seq[0];
+  h->store_valid = false;
+  h->initialized = false;
+  h->solved = false;
+  h->x0_set = false;  // the x0 row length may have changed
+  return MHPC_OK;
+}
+
+int api_get_problem_desc(Handle* h, int b, mhpc_problem_desc* desc) {
+  if (!h || !desc) return fail(MHPC_ERR_INVALID, "null argument");
+  if (b < 0 || b >= h->sp.B) return fail(MHPC_ERR_INVALID, "problem out of range");
+  *desc = h->pl[b].desc;
+  return MHPC_OK;
+}
+
+int api_num_layouts(Handle* h, int* n) {
+  if (!h || !n) return fail(MHPC_ERR_INVALID, "null argument");
+  *n = h->sp.ngrp;
+  return MHPC_OK;
+}
+
 int api_batch(Handle* h) { return h ? h->sp.B : 0; }
 
 int api_get_desc(Handle* h, mhpc_problem_desc* desc) {
   if (!h || !desc) return fail(MHPC_ERR_INVALID, "null argument");
-  *desc = h->desc;
+  *desc = h->pl[0].desc;
   return MHPC_OK;
 }
 

@@ -1,11 +1,13 @@
 // Device-side data model of the batched HSDDP solve (shared by kernels and runtime).
 //
-// HBM layout (one handle = one batch of B problems sharing a phase layout; every array is
-// problem-major so each problem's records are contiguous and a wave's loads of one knot
-// record are coalesced):
+// HBM layout (one handle = one batch of B problems; each problem has its own phase layout --
+// gait schedule -- drawn from the handle's layout table, and problems sharing a layout form a
+// group; every array is problem-major so each problem's records are contiguous and a wave's
+// loads of one knot record are coalesced):
 //   traj   [B][NSLOT][NK][KS]  x(<=14) u(4) y(4) per knot, KS = 24 doubles.  NSLOT =
 //          n_cand + 1 rollout slots; state.nom_slot names the nominal trajectory and the
-//          line-search candidates write the other slots (no copy on acceptance).
+//          line-search candidates write the other slots (no copy on acceptance).  NK is the
+//          per-problem knot stride: the largest knot count of the handle's layouts.
 //   refpos [B][NK]             forward position reference (ReferenceGen.h:94-109); the
 //          rest of the reference is constant per mode and computed in registers.
 //   K      [B][NK][56], du [B][NK][4], G [B][NK][14]   CostToGoStruct outputs per knot.
@@ -16,6 +18,9 @@
 //          are differentiated in registers by the backward kernel.
 //   px     [B][P][196]         impact Jacobian Px (column-major) at the end of WB phases.
 //   state  [B]                 ProbState (control flow + AL/ReB parameters).
+//   lay    [L]                 Layout table (read through the constant address space: scalar
+//          loads), gidx [B] the problems grouped by layout (group g = positions
+//          [go[g], go[g+1]) of gidx), lid [B] each problem's layout.
 #pragma once
 #include <stdint.h>
 
@@ -31,6 +36,8 @@ constexpr int PS = 176;       // doubles per knot in par: Jacobians + 14 cost de
                               // (lu 4, luu 4, ly 2, lyy 4 of the stance block)
 constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
+constexpr int MAXL = MHPC_MAX_LAYOUTS;  // distinct phase layouts per handle
+constexpr int ST_RMAX = 128;  // line search: staged position references per problem (knots per phase)
 constexpr int TRACE = MHPC_TRACE_LEN;
 
 // Counter slots of ProbState::cnt.  C_LS is the reference-equivalent number of serial
@@ -50,10 +57,29 @@ struct CostParams {
   real sigma0[4], delta0[4], delta_min[4], eps_tq0[4], eps_grf0[4];  // AL / ReB initial values
 };
 
-struct SolveParams {
-  int B, P, n_wb, NK;
+// Phase layout of one group of problems (MHPCLocomotion::build_problem, MHPCLocomotion.cpp
+// :63-104, for that problem's gait point): n_wb whole-body phases, then SRB phases.
+struct Layout {
+  int P, n_wb, NK;          // phases, whole-body phases, knots of this layout (<= SolveParams::NK)
   int mode[MAXP], N[MAXP], ko[MAXP], xs[MAXP];
+  int buf[MAXP];            // phase buffer of each phase (receding horizon, see k_store_*)
+  // partials work per problem and its prefix offsets per phase: WB knots with Jacobians
+  // (N - 1 per WB phase) and impact directions (14 per touchdown phase)
+  int par_knots, par_imp;
+  int par_knot_off[MAXP + 1], par_imp_off[MAXP + 1];
   real dt[MAXP];
+};
+
+struct SolveParams {
+  int B;                   // problems of the handle (the arrays' leading dimension)
+  int NK;                  // per-problem knot stride of the packed arrays (max over layouts)
+  // layout groups: the problems of group g are gidx[go[g] .. go[g + 1]) and share layout g;
+  // a launch enumerates its blocks group by group, so no block mixes layouts (kernels map a
+  // block to its group with block_group, mhpc_device.h).  ident: gidx is the identity.
+  int ngrp, ident;
+  int go[MAXL + 1];
+  int gpk[MAXL], gpi[MAXL];  // partials knot / impact work items per problem of each group
+  int pmax;                  // most phases of any layout
   real vel, height;
   int n_cand, nslot;
   real eps[MAXC];          // line-search grid 1, alpha, alpha^2, ... (host libm)
@@ -61,17 +87,15 @@ struct SolveParams {
       update_ReB;
   real eps9;               // pow(0.1, 9) (SinglePhase.cpp:202), host libm
   int AL_active, ReB_active;
-  int buf[MAXP];             // phase buffer of each phase (receding horizon, see k_store_*)
-  // partials work per problem and its prefix offsets per phase: WB knots with Jacobians
-  // (N - 1 per WB phase) and impact directions (14 per touchdown phase)
-  int par_knots, par_imp;
-  int par_knot_off[MAXP + 1], par_imp_off[MAXP + 1];
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
   int ncu, var_bws, var_ro, var_overlap;
   // line-search trials that store their running knot records (the first ro_store, and the
   // last; the rest are rolled out again when accepted -- mhpc_kernels.hip RO_STORE_FIRST)
   int ro_store;
+  // host side: some layout has both kinds of phase (the sweep can run split, bws_split) /
+  // every phase of every layout fits the line search's LDS stage of position references
+  int split_ok, stage_fits;
   // cost weights (diagonals per mode, CostBase.h:9-46 / MHPCCost.cpp:24-75) and constraint
   // parameters (ConstraintsBase.h:11-50 / MHPCConstraints.cpp:14-88): mhpc_set_cost_weights /
   // mhpc_set_constraint_params; read by every kernel from its parameter block
@@ -147,6 +171,9 @@ struct DevBufs {
   ProbState* st;
   real* out;    // export staging [B][NK][KS]
   BwsCarry* carry;  // [B]
+  const Layout* lay;  // [ngrp] layout table
+  const int* gidx;    // [B] problems grouped by layout
+  const int* lid;     // [B] layout of each problem
 };
 
 }  // namespace MHPC_NS

@@ -271,15 +271,23 @@ class MHPCLocomotion:
         capi.check(L.mhpc_create(self.desc, self._opt_c, self.batch, self.device,
                                  __import__("ctypes").byref(h)), "mhpc_create")
         self._h = h
-        n0 = self.desc.xsize(0)
+        self.descs = None  # per-problem descriptors once set_layouts mixes layouts
+        self._default_x0()
+        self.status = np.zeros(self.batch, dtype=np.int32)
+
+    def _x0_row(self) -> int:
+        ds = self.descs or [self.desc]
+        return 14 if any(d.n_wb > 0 for d in ds) else 6
+
+    def _default_x0(self):
+        n0 = self._x0_row()
         x0 = X0_DEFAULT if n0 == 14 else X0_DEFAULT[STATE_PROJ_ROWS]
         self._x0 = np.tile(x0, (self.batch, 1)).astype(np.float64)
-        self.status = np.zeros(self.batch, dtype=np.int32)
 
     # -- lifecycle ---------------------------------------------------------------------
     def set_initial_condition(self, x0: np.ndarray):
         x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(self.batch, -1))
-        if x0.shape[1] != self.desc.xsize(0):
+        if x0.shape[1] != self._x0_row():
             raise ValueError("x0 has the wrong state size for phase 0")
         self._x0 = x0
 
@@ -301,9 +309,81 @@ class MHPCLocomotion:
         g = (gait or self.gait).to_c()
         capi.check(L.mhpc_update_problem(self._h, __import__("ctypes").byref(g)),
                    "mhpc_update_problem")
+        self._refresh_descs()
+
+    # -- per-problem phase layouts: the batch axis over gait schedules ----------------------
+    def set_layouts(self, descs, layout_of_problem=None):
+        """mhpc_set_layouts: problem b gets descs[layout_of_problem[b]] (descs[b % len] when
+        None) -- each controller of the batch at its own gait / gait point, as the reference
+        builds one layout per MHPCLocomotion instance (MHPCLocomotion.cpp:63-104).  The
+        initial states return to the default; set_initial_condition + initialization follow."""
+        import ctypes
+        arr = (capi.ProblemDesc * len(descs))(*descs)
+        lop = (None if layout_of_problem is None
+               else np.ascontiguousarray(layout_of_problem, dtype=np.int32))
+        capi.check(capi.lib().mhpc_set_layouts(self._h, len(descs), arr, capi.iptr(lop)),
+                   "mhpc_set_layouts")
+        self._refresh_descs()
+        self._default_x0()
+
+    def update_problems(self, gaits, gait_of_problem=None, steps=None):
+        """Per-problem update_problem (mhpc_update_problems): problem b takes steps[b] gait
+        steps of gaits[gait_of_problem[b]] (0: keeps its layout); references follow the x0 of
+        set_initial_condition for every problem."""
+        import ctypes
+        L = capi.lib()
+        capi.check(L.mhpc_set_x0(self._h, capi.dptr(self._x0)), "mhpc_set_x0")
+        gs = (capi.GaitC * len(gaits))(*[g.to_c() for g in gaits])
+        gop = (None if gait_of_problem is None
+               else np.ascontiguousarray(gait_of_problem, dtype=np.int32))
+        st = None if steps is None else np.ascontiguousarray(steps, dtype=np.int32)
+        capi.check(L.mhpc_update_problems(self._h, len(gaits), gs, capi.iptr(gop), capi.iptr(st)),
+                   "mhpc_update_problems")
+        self._refresh_descs()
+
+    def problem_desc(self, b: int) -> capi.ProblemDesc:
+        import ctypes
         d = capi.ProblemDesc()
-        capi.check(L.mhpc_get_desc(self._h, __import__("ctypes").byref(d)), "mhpc_get_desc")
-        self.desc = d
+        capi.check(capi.lib().mhpc_get_problem_desc(self._h, int(b), ctypes.byref(d)),
+                   "mhpc_get_problem_desc")
+        return d
+
+    def num_layouts(self) -> int:
+        import ctypes
+        n = ctypes.c_int(0)
+        capi.check(capi.lib().mhpc_num_layouts(self._h, ctypes.byref(n)), "mhpc_num_layouts")
+        return n.value
+
+    def _refresh_descs(self):
+        ds = [self.problem_desc(b) for b in range(self.batch)]
+        key = lambda d: bytes(d)
+        self.descs = ds if any(key(d) != key(ds[0]) for d in ds) else None
+        self.desc = ds[0]
+
+    def get_phase_problems(self, p: int, first: int, count: int) -> dict:
+        """Phase p of problems [first, first + count) (one phase shape over the range)."""
+        d = self.descs[first] if self.descs else self.desc
+        n, N = d.xsize(p), d.N[p]
+        out = {k: np.zeros(s) for k, s in (
+            ("x", (count, N, n)), ("u", (count, N, 4)), ("y", (count, N, 4)),
+            ("K", (count, N, 4, n)), ("du", (count, N, 4)), ("Vx", (count, N, n)))}
+        capi.check(capi.lib().mhpc_get_phase_problems(
+            self._h, p, int(first), int(count),
+            *[capi.dptr(out[k]) for k in ("x", "u", "y", "K", "du", "Vx")]), "mhpc_get_phase_problems")
+        return out
+
+    def problem_concatenated(self, b: int) -> dict:
+        """Phase-concatenated arrays of one problem (the oracle's layout, row b)."""
+        d = self.descs[b] if self.descs else self.desc
+        parts = [self.get_phase_problems(p, b, 1) for p in range(d.n_phases)]
+        return {
+            "X": np.concatenate([q["x"].ravel() for q in parts]),
+            "U": np.concatenate([q["u"].ravel() for q in parts]),
+            "Y": np.concatenate([q["y"].ravel() for q in parts]),
+            "K": np.concatenate([q["K"].ravel() for q in parts]),
+            "DU": np.concatenate([q["du"].ravel() for q in parts]),
+            "G": np.concatenate([q["Vx"].ravel() for q in parts]),
+        }
 
     # MultiPhaseDDP's public members (MultiPhaseDDP.h:12-63), batched: [batch] arrays
     @property
@@ -381,7 +461,8 @@ class MHPCLocomotion:
         return out
 
     def get_scalars(self) -> dict:
-        B, P = self.batch, self.desc.n_phases
+        B = self.batch
+        P = max(d.n_phases for d in (self.descs or [self.desc]))  # rows of the most phases
         out = {"J": np.zeros(B), "dV_exp": np.zeros(B), "viol": np.zeros(B),
                "V": np.zeros((B, P)), "dV": np.zeros((B, P)),
                "trace": np.zeros((B, capi.MHPC_TRACE_LEN), dtype=np.int32)}
