@@ -207,6 +207,18 @@ struct Ldl4 {
   }
 };
 
+// Ordering point of this wave's LDS accesses for the Qxx transpose: every row's writes (and
+// the diagonal's atomic add) before the reads of the other rows' columns, and those reads
+// before the next knot's writes.  One wave's LDS operations complete in issue order, so the
+// hardware needs no wait here; the compiler must only keep the order.  Wavefront-scope fences
+// generate no instruction (AMDGPU memory model) but are acquire / release points of the C++
+// model, and the wave barrier keeps memory operations from moving across.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Per-row LDS: the knot's Q rows for the Qxx transpose, and the value function at phase
 // boundaries (row-major by state index, pitch MP reals: 16-byte aligned rows).
 constexpr int MP = sizeof(real) == 8 ? 18 : 20;
@@ -427,9 +439,11 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
     // + 2 (lxx + reg) on the diagonal of the transposed copy: an LDS atomic add, in order with
     // this wave's other LDS operations, no round trip
     atomicAdd(&rl.M[rho * MP + rho], dg2);
+    wave_lds_order();
     real T[14];
 #pragma unroll
     for (int j = 0; j < 14; ++j) T[j] = rl.M[j * MP + cr];
+    wave_lds_order();
 
     // ---- the control block on every lane ----
     wk q[4][4], Qu[4];
@@ -675,9 +689,11 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
 #pragma unroll
     for (int s = 0; s < 7; ++s) rl.M[rho * MP + wo + s] = Q[s];
     atomicAdd(&rl.M[rho * MP + (xl ? mcol(rho) : rho)], dg2);
+    wave_lds_order();
     real T[7];
 #pragma unroll
     for (int s = 0; s < 7; ++s) T[s] = rl.M[(jr + s) * MP + cr];
+    wave_lds_order();
 
     // ---- the control block on every lane (both rows alike) ----
     wk q[4][4], Qu[4];
@@ -877,9 +893,11 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
 #pragma unroll
     for (int j = 0; j < 10; ++j) rl.M[(rho & 15) * MP + j] = Q[j];
     atomicAdd(&rl.M[(rho & 15) * MP + (rho & 15)], dg2);  // see sweep_wb
+    wave_lds_order();
     real T[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) T[j] = rl.M[j * MP + cr];
+    wave_lds_order();
     real q[4][4], Qu[4];
     q[0][0] = rbc<6>(Q[6]); q[0][1] = rbc<6>(Q[7]); q[0][2] = rbc<6>(Q[8]); q[0][3] = rbc<6>(Q[9]);
     q[1][1] = rbc<7>(Q[7]); q[1][2] = rbc<7>(Q[8]); q[1][3] = rbc<7>(Q[9]);

@@ -832,6 +832,11 @@ static int solve_async(Handle* h) {
                        h->evfork,   h->evjoin, h->evpfork, h->evpjoin};
     for (const SolveOp& op : ops)
       if ((rc = issue_op(h, k, op))) {
+        // an issue failure may leave launches queued on the second / third stream (the
+        // partials fork onto stream3 and join back only at their end): drain both, so no later
+        // work on the handle runs unordered with them
+        (void)hipStreamSynchronize(h->stream3);
+        (void)hipStreamSynchronize(h->stream2);
         (void)hipStreamWaitEvent(h->stream, h->evjoin, 0);
         return rc;
       }
@@ -893,7 +898,13 @@ static int solve_async(Handle* h) {
           rc = fail(MHPC_ERR_DEVICE, "sub-batch gate record failed");
       }
     const hipError_t ej = join_all();
-    if (rc) return rc;
+    if (rc) {  // (as above: the blocks' partials streams drained on an issue failure)
+      for (int q = 0; q < nsub; ++q) {
+        (void)hipStreamSynchronize(blk[q].s3);
+        (void)hipStreamSynchronize(blk[q].s2);
+      }
+      return rc;
+    }
     HIPCHK(ej);
   }
   // totals of the per-problem counters per layout group (tiny reduction, NCNT words each)

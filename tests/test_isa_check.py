@@ -65,8 +65,13 @@ def test_no_scratch_checker(tmp_path):
     """A hot kernel with a scratch instruction or a private segment is flagged; the debug-info
     kernel (not in the solve) and kernels outside the solve are not."""
     def kern(name, body, priv):
-        return (f"{name}:\n{body}\n.Lfunc_end{name}:\n", f"  - .name: {name}\n"
-                f"    .private_segment_fixed_size: {priv}\n")
+        # descriptor block as hipcc emits it, and metadata whose ".args" entries carry ".name"s
+        # (which must not be taken for the kernel's name: ADVICE r4)
+        return (f"{name}:\n{body}\n.Lfunc_end{name}:\n"
+                f"\t.amdhsa_kernel {name}\n\t\t.amdhsa_group_segment_fixed_size 0\n"
+                f"\t\t.amdhsa_private_segment_fixed_size {priv}\n\t.end_amdhsa_kernel\n",
+                f"  - .args:\n      - .name: sp\n        .size: 8\n      - .name: d\n"
+                f"    .name: {name}\n    .private_segment_fixed_size: {priv}\n")
     parts = [kern("_ZN4mhpc9k_rolloutILb1EEEv", "\tscratch_store_dwordx2 v0, v[2:3], off", 0),
              kern("_ZN4mhpc5k_bwsILi2EEEv", "\tv_mov_b32_e32 v0, 0", 16),
              kern("_ZN4mhpc6k_initEv", "\tv_mov_b32_e32 v0, 0", 0),

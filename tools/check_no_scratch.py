@@ -18,10 +18,14 @@ COLD = ("k_cost_grad",)  # debug-info kernel (print_debugInfo), not in the solve
 def check(path):
     s = open(path).read()
     bad = []
-    for m in re.finditer(r"\.name:\s+(\S+)\n(.*?)\.private_segment_fixed_size:\s+(\d+)", s, re.S):
+    # each kernel's own descriptor block (.amdhsa_kernel <symbol> ... .end_amdhsa_kernel): the
+    # metadata's ".name:" entries also name kernel arguments, so they cannot anchor the kernel
+    for m in re.finditer(r"^\s*\.amdhsa_kernel\s+(\S+)\n(.*?)^\s*\.end_amdhsa_kernel", s, re.S | re.M):
         name = m.group(1)
-        if any(h in name for h in HOT) and not any(c in name for c in COLD) and int(m.group(3)):
-            bad.append(f"{path}: {name}: private segment {m.group(3)} bytes")
+        pm = re.search(r"\.amdhsa_private_segment_fixed_size\s+(\d+)", m.group(2))
+        priv = int(pm.group(1)) if pm else 0
+        if any(h in name for h in HOT) and not any(c in name for c in COLD) and priv:
+            bad.append(f"{path}: {name}: private segment {priv} bytes")
     for name in re.findall(r"^(_Z\S+):", s, re.M):
         if not any(h in name for h in HOT) or any(c in name for c in COLD):
             continue
