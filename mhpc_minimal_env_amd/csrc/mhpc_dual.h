@@ -85,6 +85,34 @@ MHPC_HD Dual mad(real a, real b, Dual c) { return Dual(fma(a, b, c.v), c.d); }
 MHPC_HD Dual mad(real a, Dual b, real c) { return Dual(fma(a, b.v, c), a * b.d); }
 MHPC_HD Dual mad(Dual a, real b, real c) { return Dual(fma(a.v, b, c), a.d * b); }
 
+// 1 / a of a whole-body model pivot (the 2x2 leg blocks, the 3x3 base Schur complement, the
+// 2x2 contact KKT block): on the device the hardware reciprocal estimate refined by Newton
+// steps (two in fp64, one in fp32; within an ulp of the IEEE quotient, about half the
+// instructions and dependent steps of the division sequence on the serial knot chain), the
+// estimate itself where the refinement is not finite (a = 0, +-inf, NaN: the IEEE value).
+// The single-lane, lane-pair and dual-number models all take it, so they still agree bit for
+// bit where they must (tests/test_pair_host.py, test_gpu_kernels.py).
+MHPC_HD real pivot_rcp(real a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifdef MHPC_FP32
+  const float r = __builtin_amdgcn_rcpf(a);
+  const float r1 = fmaf(r, fmaf(-a, r, 1.0f), r);
+  return __builtin_isfinite(r1) ? r1 : r;
+#else
+  const double r = __builtin_amdgcn_rcp(a);
+  const double r1 = fma(r, fma(-a, r, 1.0), r);
+  const double r2 = fma(r1, fma(-a, r1, 1.0), r1);
+  return __builtin_isfinite(r2) ? r2 : r;
+#endif
+#else
+  return real(1.0) / a;
+#endif
+}
+MHPC_HD Dual pivot_rcp(Dual a) {
+  const real r = pivot_rcp(a.v);
+  return Dual(r, -(a.d * r) * r);
+}
+
 // Scalar-generic elementary functions (real and Dual share the model source).
 MHPC_HD real val(real a) { return a; }
 MHPC_HD real val(Dual a) { return a.v; }

@@ -89,14 +89,6 @@ constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
 #ifndef MHPC_RO_PREFETCH
 #define MHPC_RO_PREFETCH 1
 #endif
-// SRB phases of the two-wave pipeline run on the dynamics wave alone (rollout, running cost,
-// record stores; one hand-over per phase): the SRB dynamics are 44 flops and 4 exact constant
-// divisions a knot, less than the ring hand-over and barrier they paid for (~2.3k cycles a
-// knot, tools/ro_timing.py).  Same arithmetic in the same order: bit for bit.
-#ifndef MHPC_RO_SRB_FUSED
-#define MHPC_RO_SRB_FUSED 1
-#endif
-constexpr bool SRB_FUSED = MHPC_RO_SRB_FUSED;
 
 // native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
 typedef real sreal2 __attribute__((ext_vector_type(2)));
@@ -238,8 +230,6 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   static_assert(RG >= 1 && (RG & (RG - 1)) == 0, "ring depth");
   __shared__ real ring[RD][RING_W][64];
   __shared__ acc sJ[64], sViol[64], sV[MAXP][64];
-  __shared__ acc sVF[SRB_FUSED && PIPE ? 64 : 1];  // an SRB phase's value, dynamics -> cost wave
-  __shared__ real sRefF[SRB_FUSED && PIPE && ST ? SNP : 1][SRB_FUSED && PIPE && ST ? ST_RMAX + 1 : 1];
   __shared__ real sH[MAXP][64];
   __shared__ int sAny;
   __shared__ int sNom[ST ? ST_PPW : 1], sProb[ST ? ST_PPW : 1];
@@ -381,7 +371,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   };
   // dynamics side, knot k of phase p: u = (u_nom + eps du) + K (x - x_nom), x+ = x + dt f(x, u);
   // rr = the knot's record (x, u, y) as the ring / the cost side takes it
-  auto dyn_knot = [&](auto WBc, int p, int k, real* rr, bool halve = true) __attribute__((always_inline)) {
+  auto dyn_knot = [&](auto WBc, int p, int k, real* rr) __attribute__((always_inline)) {
     const int mode = L.mode[p], ko = L.ko[p];
     const real dt = L.dt[p];
     constexpr bool wb = decltype(WBc)::value;
@@ -447,7 +437,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       for (int i = 0; i < 6; ++i) rr[i] = x[i];
 #pragma unroll
       for (int i = 0; i < 4; ++i) { rr[6 + i] = u[i]; rr[10 + i] = real(0.0); }
-      if (PAIR && halve) {  // the pair splits the 14 record entries: 0..6 even lane, 7..13 odd
+      if (PAIR) {  // the pair splits the 14 record entries: 0..6 even lane, 7..13 odd
 #pragma unroll
         for (int i = 0; i < 7; ++i) rr[i] = back ? rr[7 + i] : rr[i];
       }
@@ -636,72 +626,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         }
         __syncthreads();
       };
-      // SRB phase on the dynamics wave alone (SRB_FUSED): each knot's record goes to the
-      // running cost and the store here; the phase value to the cost wave at the phase end
-      auto dyn_srb_phase = [&](int p) __attribute__((always_inline)) {
-        MHPC_NO_FMA_COST
-        using WBc = std::false_type;
-        const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
-        const real dt = L.dt[p];
-        constexpr int CH = Stage<false>::CH;
-        dyn_phase_begin(WBc{}, p);
-        // the phase's position references: into this wave's own stage (the cost wave may still
-        // read its stage for the phase before)
-        const real* rpos = d.refpos + (size_t)(in ? b : 0) * sp.NK + ko;
-        if constexpr (ST) {
-#pragma unroll
-          for (int i = 0; i < SNP * ST_RMAX / 64; ++i) {
-            const int fi = lane + 64 * i, rl = fi / ST_RMAX, rk = fi - rl * ST_RMAX;
-            if (rk < N && nomv[rl] >= 0) sRefF[rl][rk] = d.refpos[(size_t)pbv[rl] * sp.NK + ko + rk];
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (one wave: in order)
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        const real refT = run ? rpos[N - 1] : real(0.0);
-        // RO_STORE_FIRST as store_rec; the pair's even lane stores the whole record (both
-        // lanes hold it)
-        const bool stores = (j < sp.ro_store || j == nc - 1) && !(PAIR && back);
-        acc V = 0;
-        for (int k = 0; k < N - 1; ++k) {
-          RO_T(tk0);
-          if (ST && !PF && (k & (CH - 1)) == 0) chunk_turn(false, ko, N, k);
-          real rr[RING_W];
-          if (run) dyn_knot(WBc{}, p, k, rr, false);
-          if (PF && k + 1 < N - 1) {
-            if (((k + 1) & (CH - 1)) == 0) chunk_turn(false, ko, N, k + 1);
-            if (run) prefetch(false, k + 1);
-          }
-          if (run) {
-            const real pos = ST ? sRefF[lp][k] : rpos[k];
-            V += fb_running_cost(sp, mode, dt, pos, rr, rr + 6);
-            if (stores) {
-              real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, ko + k));
-#pragma unroll
-              for (int i = 0; i < 7; ++i) o[i] = real2{rr[2 * i], rr[2 * i + 1]};
-            }
-          }
-#ifdef MHPC_RO_TIMING
-          if (lane == 0 && run) {
-            ro_cyc[3] += clock64() - tk0;
-            ro_cyc[5]++;
-          }
-#endif
-        }
-        if (run) {  // terminal cost and state (every trial stores it), the phase value
-          V += srb_terminal_cost(mode, refT, x);
-          if (!PAIR || !back) {
-            real2* o = reinterpret_cast<real2*>(traj_ptr(sp, d, b, slot, ko + N - 1));
-#pragma unroll
-            for (int i = 0; i < 3; ++i) o[i] = real2{x[2 * i], x[2 * i + 1]};
-          }
-          if (!PAIR || !back) sVF[cl] = V;
-        }
-        __syncthreads();
-      };
       for (int p = 0; p < L.P; ++p) {
         if (p < L.n_wb) dyn_phase(std::true_type{}, p);
-        else if (SRB_FUSED) dyn_srb_phase(p);
         else dyn_phase(std::false_type{}, p);
       }
     } else {
@@ -755,22 +681,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
           cost_terminal(WBc, p, c, r, V);
         }
       };
-      // an SRB phase the dynamics wave ran alone (SRB_FUSED): its value at the phase end,
-      // accumulated exactly as cost_terminal does (h = 0 in SRB phases)
-      auto cost_srb_phase = [&](int p) __attribute__((always_inline)) {
-        __syncthreads();
-        if (run) {
-          const acc V = sVF[lane];
-          const real h = 0;
-          J += V;
-          viol2 += acc(h) * h;
-          sV[p][lane] = V;
-          sH[p][lane] = h;
-        }
-      };
       for (int p = 0; p < L.P; ++p) {
         if (p < L.n_wb) cost_phase(std::true_type{}, p);
-        else if (SRB_FUSED) cost_srb_phase(p);
         else cost_phase(std::false_type{}, p);
       }
     }

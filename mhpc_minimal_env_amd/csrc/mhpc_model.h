@@ -246,7 +246,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   for (int l = 0; l < 2; ++l) {
     const int i0 = 3 + 2 * l, i1 = 4 + 2 * l;
     const S a = M[tri(i0, i0)], b = M[tri(i1, i0)], c = M[tri(i1, i1)];
-    const S rdet = S(real(1.0)) / mad(a, c, -(b * b));
+    const S rdet = pivot_rcp(mad(a, c, -(b * b)));
     F.Li[l][0] = c * rdet;
     F.Li[l][1] = -b * rdet;
     F.Li[l][2] = a * rdet;
@@ -277,7 +277,7 @@ MHPC_HD void arrow_factor(const S M[28], ArrowFactor<S>& F) {
   const S c00 = mad(s11, s22, -(s21 * s21));
   const S c10 = mad(s21, s20, -(s10 * s22));
   const S c20 = mad(s10, s21, -(s11 * s20));
-  const S rdet = S(real(1.0)) / mad(s20, c20, mad(s10, c10, s00 * c00));
+  const S rdet = pivot_rcp(mad(s20, c20, mad(s10, c10, s00 * c00)));
   F.Si[0] = c00 * rdet;
   F.Si[1] = c10 * rdet;
   F.Si[2] = mad(s00, s22, -(s20 * s20)) * rdet;
@@ -359,7 +359,7 @@ MHPC_HD void kkt_contact(const Q M[28], const ArrowFactor<Q>& F, const Q J[2][7]
     r0 = mad(-J[0][i], v[i], r0);
     r1 = mad(-J[1][i], v[i], r1);
   }
-  const Q rdet = Q(real(1.0)) / mad(A00, A11, -(A01 * A01));
+  const Q rdet = pivot_rcp(mad(A00, A11, -(A01 * A01)));
   lam[0] = mad(A11, r0, -(A01 * r1)) * rdet;
   lam[1] = mad(A00, r1, -(A01 * r0)) * rdet;
 #pragma unroll
@@ -465,7 +465,7 @@ MHPC_HD void wb_knot_primal(const real* x, const real* u, WbKnot& K) {
       r1 = mad(-K.J[1][i], v[i], r1);
     }
     K.A00 = A00; K.A01 = A01; K.A11 = A11;
-    K.rdet = real(1.0) / mad(A00, A11, -(A01 * A01));
+    K.rdet = pivot_rcp(mad(A00, A11, -(A01 * A01)));
     K.lam[0] = mad(A11, r0, -(A01 * r1)) * K.rdet;
     K.lam[1] = mad(A00, r1, -(A01 * r0)) * K.rdet;
 #pragma unroll

@@ -43,6 +43,39 @@ MHPC_HD float pair_swap(float v) {
 #endif
 }
 
+// value held by the pair's even (E = 0) / odd (E = 1) lane, on both lanes: DPP quad_perm
+// [0, 0, 2, 2] / [1, 1, 3, 3] -- a broadcast inside the pair, no lane-dependent select
+template <int E>
+MHPC_HD double pair_from(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int ctl = E ? 0xF5 : 0xA0;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, ctl, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), ctl, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+#else
+  return v;  // (host: only the lane-parity forms below are used)
+#endif
+}
+template <int E>
+MHPC_HD float pair_from(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), E ? 0xF5 : 0xA0, 0xF, 0xF, false));
+#else
+  return v;
+#endif
+}
+// The stance lane's value (odd lane when sback) on both lanes; `mine` = this lane is it.
+template <bool SBACK>
+MHPC_HD real pair_stance(bool mine, real v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return pair_from<SBACK ? 1 : 0>(v);
+#else
+  const real o = pair_swap(v);
+  return mine ? v : o;
+#endif
+}
+
 // Jacobian of a point of the own leg (leg_point_jac with the hip side as data: sg = +1
 // front, -1 back), same expressions.
 MHPC_HD void pair_point_jac(const LegGeo<real, real>& L, real sg, real sth,
@@ -124,11 +157,18 @@ MHPC_HD void pair_leg_mass_bias(const LegGeo<real, real>& L, real sg, real sth,
   o.hk = hl[4];
 }
 
-// Order the own / partner value of a per-leg quantity as (front, back).
+// Order the own / partner value of a per-leg quantity as (front, back): the even (front)
+// lane's and the odd (back) lane's value, broadcast inside the pair.
 MHPC_HD void pair_order(bool back, real own, real* fr, real* bk) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  (void)back;
+  *fr = pair_from<0>(own);
+  *bk = pair_from<1>(own);
+#else
   const real oth = pair_swap(own);
   *fr = back ? oth : own;
   *bk = back ? own : oth;
+#endif
 }
 
 // front + back of a per-leg quantity, the same on both lanes without ordering them: a sum
@@ -164,6 +204,10 @@ MHPC_HD void pair_solve(const PairFactor& F, bool back, const real rb[3],
   xl[0] = w0 - mad(F.Z[0][2], x2, mad(F.Z[0][1], x1, F.Z[0][0] * x0));
   xl[1] = w1 - mad(F.Z[1][2], x2, mad(F.Z[1][1], x1, F.Z[1][0] * x0));
 }
+
+template <bool SBACK>
+MHPC_HD void wb_stance_pair(const real* x, const LegGeo<real, real>& L, real sg, real sth,
+                            real cth, bool back, const PairFactor& F, real v[7], real* y);
 
 // x (14, identical on both lanes of the pair), u_own = the own leg's two joint torques.
 // Returns xdot (14) and y (4), identical on both lanes.  mode as wb_dynamics.
@@ -204,7 +248,7 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   PairFactor F;
   {
     const real a = lm.Mhh, b = lm.Mkh, c = lm.Mkk;
-    const real rdet = real(1.0) / mad(a, c, -(b * b));
+    const real rdet = pivot_rcp(mad(a, c, -(b * b)));
     F.Li[0] = c * rdet;
     F.Li[1] = -b * rdet;
     F.Li[2] = a * rdet;
@@ -230,7 +274,7 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
     const real c00 = mad(s11, s22, -(s21 * s21));
     const real c10 = mad(s21, s20, -(s10 * s22));
     const real c20 = mad(s10, s21, -(s11 * s20));
-    const real rdet = real(1.0) / mad(s20, c20, mad(s10, c10, s00 * c00));
+    const real rdet = pivot_rcp(mad(s20, c20, mad(s10, c10, s00 * c00)));
     F.Si[0] = c00 * rdet;
     F.Si[1] = c10 * rdet;
     F.Si[2] = mad(s00, s22, -(s20 * s20)) * rdet;
@@ -252,10 +296,24 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   pair_order(back, vl[1], &v[4], &v[6]);
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = real(0.0);
-  if (mode == 1 || mode == 3) {
-    // stance foot (mode 1: back, mode 3: front): its lane evaluates the foot Jacobian and
-    // J-dot qdot (wb_foot_jac_full), the partner takes them by swap
-    const bool sback = mode == 1;
+  if (mode == 1) wb_stance_pair<true>(x, L, sg, sth, cth, back, F, v, y);
+  else if (mode == 3) wb_stance_pair<false>(x, L, sg, sth, cth, back, F, v, y);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    xdot[i] = x[7 + i];
+    xdot[7 + i] = v[i];
+  }
+}
+
+// The contact KKT correction of a stance mode (kkt_contact), SBACK = the back foot is down
+// (mode 1; the front foot: mode 3): the stance foot's lane evaluates the foot Jacobian and
+// J-dot qdot (wb_foot_jac_full), broadcast to the partner.
+template <bool SBACK>
+MHPC_HD void wb_stance_pair(const real* x, const LegGeo<real, real>& L, real sg, real sth,
+                            real cth, bool back, const PairFactor& F, real v[7], real* y) {
+  MHPC_NO_FMA_WB
+  {
+    const bool sback = SBACK;
     const bool mine = sback == back;
     real jx[5], jz[5], jdx, jdz;
     pair_point_jac(L, sg, sth, cth, kThighLen, kShankLen, jx, jz, &jdx, &jdz);
@@ -266,21 +324,16 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
     real Jb[2][3], Jl[2][2];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      const real ox = pair_swap(jx[a]), oz = pair_swap(jz[a]);
-      Jb[0][a] = mine ? jx[a] : ox;
-      Jb[1][a] = mine ? jz[a] : oz;
+      Jb[0][a] = pair_stance<SBACK>(mine, jx[a]);
+      Jb[1][a] = pair_stance<SBACK>(mine, jz[a]);
     }
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      const real ox = pair_swap(jx[3 + a]), oz = pair_swap(jz[3 + a]);
-      Jl[0][a] = mine ? jx[3 + a] : ox;
-      Jl[1][a] = mine ? jz[3 + a] : oz;
+      Jl[0][a] = pair_stance<SBACK>(mine, jx[3 + a]);
+      Jl[1][a] = pair_stance<SBACK>(mine, jz[3 + a]);
     }
-    {
-      const real o0 = pair_swap(jd0), o1 = pair_swap(jd1);
-      jd0 = mine ? jd0 : o0;
-      jd1 = mine ? jd1 : o1;
-    }
+    jd0 = pair_stance<SBACK>(mine, jd0);
+    jd1 = pair_stance<SBACK>(mine, jd1);
     // full J rows in model order (zeros on the swing leg's columns)
     real J[2][7];
 #pragma unroll
@@ -314,18 +367,13 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
       r0 = mad(-J[0][i], v[i], r0);
       r1 = mad(-J[1][i], v[i], r1);
     }
-    const real rdet = real(1.0) / mad(A00, A11, -(A01 * A01));
+    const real rdet = pivot_rcp(mad(A00, A11, -(A01 * A01)));
     const real lam0 = mad(A11, r0, -(A01 * r1)) * rdet;
     const real lam1 = mad(A00, r1, -(A01 * r0)) * rdet;
 #pragma unroll
     for (int i = 0; i < 7; ++i) v[i] += mad(Y[0][i], lam0, Y[1][i] * lam1);
     y[sback ? 2 : 0] = lam0;
     y[sback ? 3 : 1] = lam1;
-  }
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    xdot[i] = x[7 + i];
-    xdot[7 + i] = v[i];
   }
 }
 
