@@ -5,8 +5,10 @@
  * -> HSDDPSolver/source/MultiPhaseDDP.cpp:154-289).  Plain C types only: pointers, sizes,
  * POD structs; no exceptions cross the ABI; every entry point returns an mhpc_status
  * (0 = OK).  One handle owns the device-resident state of a BATCH of independent MPC
- * problems that share one phase layout (gait schedule).  Calls on one handle are
- * serialised by the caller; different handles (devices, streams) are independent.
+ * problems; each problem has its own phase layout (gait schedule) drawn from a table of up to
+ * MHPC_MAX_LAYOUTS distinct layouts (mhpc_set_layouts; by default every problem has the
+ * layout given at create).  Calls on one handle are serialised by the caller; different
+ * handles (devices, streams) are independent.
  *
  * Reference interfaces replaced (file:line in /root/reference):
  *   mhpc_create          MHPCLocomotion ctor + memory_alloc      (MHPCLocomotion.cpp:8-43,218-261)
@@ -27,6 +29,11 @@
  *                        _tconstr_violation and SinglePhaseAbstract::_V/_dV
  *                        (MultiPhaseDDP.h:57-60, SinglePhaseAbstract.h:116-118)
  *   mhpc_destroy         MHPCLocomotion::~MHPCLocomotion / memory_free (MHPCLocomotion.cpp:383-470)
+ *   mhpc_update_problem  MHPCLocomotion::update_problem          (MHPCLocomotion.cpp:107-158,
+ *                        Gait.h:21-77): gait advance, phase-buffer rotation, re-init
+ *   mhpc_set_layouts     one MHPCLocomotion per controller, each built from its own Gait
+ *                        (MHPCLocomotion.cpp:63-104): per-problem phase layouts in one batch
+ *   mhpc_update_problems update_problem of every controller with its own gait and step count
  */
 #ifndef MHPC_CAPI_H
 #define MHPC_CAPI_H

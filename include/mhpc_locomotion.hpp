@@ -18,9 +18,11 @@
 // Header-only; link with -lmhpc_amd.  Errors throw std::runtime_error on this side of
 // the ABI (none cross it).
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstddef>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <memory>
 #include <stdexcept>
@@ -219,21 +221,7 @@ class MHPCLocomotion {
       : batch_(batch) {
     static_assert(sizeof(TH) == 8, "only the double instantiation exists (as in the reference)");
     const int np = params->n_wbphase + params->n_fbphase;
-    desc_ = mhpc_problem_desc{};
-    desc_.n_wb = params->n_wbphase;
-    desc_.n_fb = params->n_fbphase;
-    desc_.dt_wb = (double)params->dt_wb;
-    desc_.dt_fb = (double)params->dt_fb;
-    desc_.vel_cmd = params->usrcmd ? params->usrcmd->vel : 0.f;
-    desc_.height_cmd = params->usrcmd ? params->usrcmd->height : 0.f;
-    desc_.precision = 64;
-    const std::vector<int> seq = gait->get_mode_seq(params->cmode, np);
-    const std::vector<float> tim = gait->get_timings(seq);
-    for (int p = 0; p < np && p < MHPC_MAX_PHASES; ++p) {  // build_problem (:63-104)
-      desc_.mode_seq[p] = seq[p];
-      // float timing / (double)(float dt), as the reference's DVec<float> / double member
-      desc_.N[p] = (int)std::round((double)tim[p] / (p < desc_.n_wb ? desc_.dt_wb : desc_.dt_fb));
-    }
+    desc_ = build_desc(params, gait);
     opt_ = mhpc_hsddp_option{option.alpha, option.gamma, option.update_penalty,
                              option.update_relax, option.update_regularization,
                              option.update_ReB, option.max_DDP_iter, option.max_AL_iter,
@@ -242,30 +230,48 @@ class MHPCLocomotion {
     check(mhpc_create(&desc_, &opt_, batch_, device, &h_), "mhpc_create");
     _option = option;
     _n_phases = np;
-    for (int p = 0; p < np; ++p) phase_store_.emplace_back(new SinglePhaseAbstract<TH>());
-    for (auto& q : phase_store_) _phases.push_back(q.get());
-    refresh_phases(false);
     gait_ = gait->to_c();
     // default initial condition (MHPCLocomotion.cpp:37-39), projected if phase 0 is SRB
     const double x0[14] = {0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098,
                            0.9011, 0.2756,  0.7333,  0.0446, 0.0009,  1.3219, 2.7346};
-    const int n0 = desc_.n_wb > 0 ? 14 : 6;
-    const int proj[6] = {0, 1, 2, 7, 8, 9};
-    x0_.resize((size_t)batch_ * n0);
-    for (int b = 0; b < batch_; ++b)
-      for (int i = 0; i < n0; ++i) x0_[(size_t)b * n0 + i] = n0 == 14 ? x0[i] : x0[proj[i]];
+    xw_ = desc_.n_wb > 0 ? 14 : 6;
+    pmax_ = np;
+    refresh_phases(false);
+    default_x0();
   }
   ~MHPCLocomotion() { mhpc_destroy(h_); }
+  // the phase layout MHPCLocomotion::build_problem makes (MHPCLocomotion.cpp:63-104) for the
+  // controller's parameters and gait at its current mode params->cmode
+  static mhpc_problem_desc build_desc(const MHPCUserParameters* params, Gait* gait) {
+    const int np = params->n_wbphase + params->n_fbphase;
+    mhpc_problem_desc d{};
+    d.n_wb = params->n_wbphase;
+    d.n_fb = params->n_fbphase;
+    d.dt_wb = (double)params->dt_wb;
+    d.dt_fb = (double)params->dt_fb;
+    d.vel_cmd = params->usrcmd ? params->usrcmd->vel : 0.f;
+    d.height_cmd = params->usrcmd ? params->usrcmd->height : 0.f;
+    d.precision = 64;
+    const std::vector<int> seq = gait->get_mode_seq(params->cmode, np);
+    const std::vector<float> tim = gait->get_timings(seq);
+    for (int p = 0; p < np && p < MHPC_MAX_PHASES; ++p) {
+      d.mode_seq[p] = seq[p];
+      // float timing / (double)(float dt), as the reference's DVec<float> / double member
+      d.N[p] = (int)std::round((double)tim[p] / (p < d.n_wb ? d.dt_wb : d.dt_fb));
+    }
+    return d;
+  }
   MHPCLocomotion(const MHPCLocomotion&) = delete;
   MHPCLocomotion& operator=(const MHPCLocomotion&) = delete;
 
-  // extension: per-problem initial states [batch][xsize of phase 0]
+  // extension: per-problem initial states [batch][x0_width()] (14 when any problem has a
+  // whole-body phase -- an SRB-only problem reads the first 6 of its row -- else 6)
   void set_initial_conditions(const std::vector<double>& x0) { x0_ = x0; }
+  int x0_width() const { return xw_; }
   // MultiPhaseDDP::set_initial_condition for every problem of the batch (same state)
   void set_initial_condition(const std::vector<double>& x0) {
-    const int n0 = desc_.n_wb > 0 ? 14 : 6;
     for (int b = 0; b < batch_; ++b)
-      for (int i = 0; i < n0; ++i) x0_[(size_t)b * n0 + i] = x0[i];
+      for (int i = 0; i < xw_; ++i) x0_[(size_t)b * xw_ + i] = x0[i];
   }
 
   // MHPCLocomotion::update_problem (MHPCLocomotion.cpp:107-158): gait advances one mode,
@@ -273,8 +279,45 @@ class MHPCLocomotion {
   void update_problem() {
     check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
     check(mhpc_update_problem(h_, &gait_), "mhpc_update_problem");
-    check(mhpc_get_desc(h_, &desc_), "mhpc_get_desc");
-    refresh_phases(false);
+    refresh_descs();
+  }
+
+  // extension: per-problem phase layouts in one batch -- one MHPCLocomotion per controller
+  // in the reference, each built from its own Gait / gait point (MHPCLocomotion.cpp:63-104).
+  // Problem b gets descs[layout_of_problem[b]] (descs[b % n] for an empty vector); the
+  // initial states return to the default, initialization() precedes the next solve.
+  void set_layouts(const std::vector<mhpc_problem_desc>& descs,
+                   const std::vector<int32_t>& layout_of_problem = {}) {
+    check(mhpc_set_layouts(h_, (int)descs.size(), descs.data(),
+                           layout_of_problem.empty() ? nullptr : layout_of_problem.data()),
+          "mhpc_set_layouts");
+    refresh_descs();
+    default_x0();
+  }
+  // extension: update_problem per controller -- problem b takes steps[b] gait steps of
+  // gaits[gait_of_problem[b]] (0: keeps its layout and warm start); empty vectors: gaits[0]
+  // for every problem, one step each
+  void update_problems(const std::vector<Gait*>& gaits,
+                       const std::vector<int32_t>& gait_of_problem = {},
+                       const std::vector<int32_t>& steps = {}) {
+    std::vector<mhpc_gait> gs;
+    for (Gait* g : gaits) gs.push_back(g->to_c());
+    check(mhpc_set_x0(h_, x0_.data()), "mhpc_set_x0");
+    check(mhpc_update_problems(h_, (int)gs.size(), gs.data(),
+                               gait_of_problem.empty() ? nullptr : gait_of_problem.data(),
+                               steps.empty() ? nullptr : steps.data()),
+          "mhpc_update_problems");
+    refresh_descs();
+  }
+  mhpc_problem_desc problem_desc(int b) {
+    mhpc_problem_desc d{};
+    check(mhpc_get_problem_desc(h_, b, &d), "mhpc_get_problem_desc");
+    return d;
+  }
+  int num_layouts() {
+    int n = 0;
+    check(mhpc_num_layouts(h_, &n), "mhpc_num_layouts");
+    return n;
   }
 
   // execution horizon of solve_mhpc (ms_exec / CTG_exec, MHPCLocomotion.cpp:176-194): nominal
@@ -326,6 +369,7 @@ class MHPCLocomotion {
   void select_problem(int b) {
     if (b < 0 || b >= batch_) throw std::runtime_error("select_problem: no such problem");
     problem_ = b;
+    if (!pdesc_.empty()) desc_ = pdesc_[b];
     refresh_phases(solved_);
   }
 
@@ -335,24 +379,19 @@ class MHPCLocomotion {
   // control / gradient / cost (exact for n_wbphase = 2; rows past an SRB phase's own N are
   // the zero-initialised buffer; clamped where the reference would read past the array).
   void print_debugInfo(int problem = 0) {
-    const int nwb = desc_.n_wb, nfb = desc_.n_fb, np = nwb + nfb;
+    const mhpc_problem_desc dsc = pdesc_.empty() ? desc_ : pdesc_[problem];
+    const int nwb = dsc.n_wb, nfb = dsc.n_fb, np = nwb + nfb;
     struct Part { int n, N; std::vector<double> x, u, g, lx, phix; };
     std::vector<Part> parts(np);
     for (int p = 0; p < np; ++p) {
       Part& q = parts[p];
-      check(mhpc_phase_dims(&desc_, p, &q.n, &q.N), "mhpc_phase_dims");
-      std::vector<double> x((size_t)batch_ * q.N * q.n), u((size_t)batch_ * q.N * 4),
-          g((size_t)batch_ * q.N * q.n), lx((size_t)batch_ * (q.N - 1) * q.n),
-          ph((size_t)batch_ * q.n);
-      check(mhpc_get_phase(h_, p, x.data(), u.data(), nullptr, nullptr, nullptr, g.data()),
-            "mhpc_get_phase");
-      check(mhpc_get_cost_gradients(h_, p, lx.data(), ph.data()), "mhpc_get_cost_gradients");
-      const size_t b = (size_t)problem;
-      q.x.assign(x.begin() + b * q.N * q.n, x.begin() + (b + 1) * q.N * q.n);
-      q.u.assign(u.begin() + b * q.N * 4, u.begin() + (b + 1) * q.N * 4);
-      q.g.assign(g.begin() + b * q.N * q.n, g.begin() + (b + 1) * q.N * q.n);
-      q.lx.assign(lx.begin() + b * (q.N - 1) * q.n, lx.begin() + (b + 1) * (q.N - 1) * q.n);
-      q.phix.assign(ph.begin() + b * q.n, ph.begin() + (b + 1) * q.n);
+      check(mhpc_phase_dims(&dsc, p, &q.n, &q.N), "mhpc_phase_dims");
+      q.x.resize((size_t)q.N * q.n); q.u.resize((size_t)q.N * 4); q.g.resize((size_t)q.N * q.n);
+      q.lx.resize((size_t)(q.N - 1) * q.n); q.phix.resize(q.n);
+      check(mhpc_get_phase_problems(h_, p, problem, 1, q.x.data(), q.u.data(), nullptr, nullptr,
+                                    nullptr, q.g.data()), "mhpc_get_phase_problems");
+      check(mhpc_get_cost_gradients_problems(h_, p, problem, 1, q.lx.data(), q.phix.data()),
+            "mhpc_get_cost_gradients_problems");
     }
     auto n_rows = [&](int i) { return i + 2 < np ? parts[i + 2].N : parts[nwb + i].N; };
     // rows k < want of a [N][w] block, zero rows past N
@@ -417,11 +456,45 @@ class MHPCLocomotion {
   HSDDP_OPTION<TH> _option;
 
  private:
-  // phase configuration from the handle's current layout; costs from the last solve
+  // every problem's layout (kept only when they differ), the x0 row width, the widest
+  // phase count (the row width of mhpc_get_scalars' per-phase arrays)
+  void refresh_descs() {
+    std::vector<mhpc_problem_desc> ds(batch_);
+    bool mixed = false;
+    for (int b = 0; b < batch_; ++b) {
+      ds[b] = problem_desc(b);
+      mixed = mixed || std::memcmp(&ds[b], &ds[0], sizeof(mhpc_problem_desc)) != 0;
+    }
+    xw_ = 6;
+    pmax_ = 0;
+    for (const mhpc_problem_desc& d : ds) {
+      if (d.n_wb > 0) xw_ = 14;
+      pmax_ = std::max(pmax_, d.n_wb + d.n_fb);
+    }
+    desc_ = ds[problem_];
+    pdesc_ = mixed ? std::move(ds) : std::vector<mhpc_problem_desc>();
+    refresh_phases(false);
+  }
+  // the reference's default initial condition (MHPCLocomotion.cpp:37-39), projected for a
+  // batch without whole-body phases
+  void default_x0() {
+    const double x0[14] = {0.0927, -0.1093, -0.1542, 1.0957, -2.2033, 0.9742, -1.7098,
+                           0.9011, 0.2756,  0.7333,  0.0446, 0.0009,  1.3219, 2.7346};
+    const int proj[6] = {0, 1, 2, 7, 8, 9};
+    x0_.resize((size_t)batch_ * xw_);
+    for (int b = 0; b < batch_; ++b)
+      for (int i = 0; i < xw_; ++i) x0_[(size_t)b * xw_ + i] = xw_ == 14 ? x0[i] : x0[proj[i]];
+  }
+  // phase configuration from the selected problem's current layout; costs from the last solve
   void refresh_phases(bool scalars) {
     const int np = desc_.n_wb + desc_.n_fb;
-    std::vector<double> J(batch_), dV(batch_), viol(batch_), Vp((size_t)batch_ * np),
-        dVp((size_t)batch_ * np);
+    while ((int)phase_store_.size() < np) phase_store_.emplace_back(new SinglePhaseAbstract<TH>());
+    _phases.clear();
+    for (int p = 0; p < np; ++p) _phases.push_back(phase_store_[p].get());
+    _n_phases = np;
+    const size_t pw = (size_t)pmax_;
+    std::vector<double> J(batch_), dV(batch_), viol(batch_), Vp((size_t)batch_ * pw),
+        dVp((size_t)batch_ * pw);
     if (scalars)
       check(mhpc_get_scalars(h_, J.data(), dV.data(), viol.data(), Vp.data(), dVp.data(), nullptr),
             "mhpc_get_scalars");
@@ -437,8 +510,8 @@ class MHPCLocomotion {
       q._dt = p < desc_.n_wb ? desc_.dt_wb : desc_.dt_fb;
       q._N_TIMESTEPS = desc_.N[p];
       q._xsize = p < desc_.n_wb ? 14 : 6;
-      q._V = scalars ? (TH)Vp[(size_t)problem_ * np + p] : TH(0);
-      q._dV = scalars ? (TH)dVp[(size_t)problem_ * np + p] : TH(0);
+      q._V = scalars ? (TH)Vp[(size_t)problem_ * pw + p] : TH(0);
+      q._dV = scalars ? (TH)dVp[(size_t)problem_ * pw + p] : TH(0);
     }
     if (scalars) {
       _actual_cost = J[problem_];
@@ -477,6 +550,8 @@ class MHPCLocomotion {
   std::vector<double> x0_;
   std::vector<int32_t> status_;
   std::vector<std::unique_ptr<SinglePhaseAbstract<TH>>> phase_store_;
+  std::vector<mhpc_problem_desc> pdesc_;  // per-problem layouts (empty: all equal desc_)
+  int xw_ = 14, pmax_ = 0;
   int problem_ = 0;
   bool solved_ = false;
 };

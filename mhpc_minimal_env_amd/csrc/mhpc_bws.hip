@@ -303,12 +303,13 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
     const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
     pxn = tk[xi];
     ppos = pos[k];
-    const real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-    pcv = rec[PS_JAC + cq];
+    pcv = d.par[par_jac(sp.NK, b, ko + k) + cq];
+    const real* r1 = d.par + par_col(sp.NK, b, c1, ko + k);
+    const real* r2 = d.par + par_col(sp.NK, b, c2, ko + k);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pr1[r] = rec[c1 * 9 + r];
+    for (int r = 0; r < NR; ++r) pr1[r] = r1[r];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pr2[r] = rec[c2 * 9 + r];
+    for (int r = 0; r < NR; ++r) pr2[r] = r2[r];
   };
   real H[14], Gv;
   {
@@ -568,14 +569,16 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
     const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
     pxn = tk[xi];
     ppos = pos[k];
-    const real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-    pcv = rec[PS_JAC + cq];
+    pcv = d.par[par_jac(sp.NK, b, ko + k) + cq];
+    const real* r1 = d.par + par_col(sp.NK, b, rho, ko + k);
+    const real* rb = d.par + par_col(sp.NK, b, cb, ko + k);
+    const real* r2 = d.par + par_col(sp.NK, b, c2, ko + k);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pr1[r] = rec[rho * 9 + r];
+    for (int r = 0; r < NR; ++r) pr1[r] = r1[r];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) prb[r] = rec[cb * 9 + r];
+    for (int r = 0; r < NR; ++r) prb[r] = rb[r];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pr2[r] = rec[c2 * 9 + r];
+    for (int r = 0; r < NR; ++r) pr2[r] = r2[r];
   };
   real H[14], Gv;
   {
@@ -877,12 +880,13 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
     for (int c = 3; c < 6; ++c) S[c] = dt * H[c - 3];
 #pragma unroll
     for (int c = 6; c < 10; ++c) S[c] = real(0.0);
-    srb_s_a(S[0], S[1], S[2], S[3], S[4], W, H + 3);
+    // (only the structurally non-zero W terms: W is 5 + 8 non-zeros, FBDynamics_par.c:53-54)
+    srb_sp_a(S[0], S[1], S[3], S[4], W, H + 3);
     real Q[10], Qv1;
 #pragma unroll
     for (int c = 0; c < 5; ++c) Q[c] = coef * qperm(S[c]);
     sb_odd3_5(Q[0], Q[1], Q[2], Q[3], Q[4], S + 0, W);
-    srb_s_b(S[5], S[6], S[7], S[8], S[9], W, H + 3);
+    srb_sp_b(S[5], S[6], S[7], S[8], S[9], W, H + 3);
 #pragma unroll
     for (int c = 5; c < 10; ++c) Q[c] = coef * qperm(S[c]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
@@ -1161,10 +1165,13 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
 // idle).  RPP = 2 (RPW = 2): problem q on rows 2q, 2q+1 sharing one RowLds (sweep_wb2).
 //
 // PART 0: the whole sweep with its regularisation retries (MultiPhaseDDP.cpp:196-241).
-// PART 1: the SRB phases of the first attempt only, the value function at the WB boundary
-// saved to d.carry (this launch runs beside the partials, which it does not read).
-// PART 2: the WB phases of the first attempt (rows whose SRB part passed), then the same
-// retries as PART 0 (whole sweeps) -- the same attempts with the same regularisation.
+// PART 1: the SRB phases of the attempts until one passes them (an attempt that fails there
+// never reaches a WB phase, so it is wholly done here: with the reference's default weights the
+// first DDP iteration of every AL iteration fails its first attempt at the first knot), the
+// value function at the WB boundary saved to d.carry (this launch runs beside the partials,
+// which it does not read).
+// PART 2: the WB phases of that attempt, then the same retries as PART 0 (whole sweeps) --
+// the same attempts with the same regularisation, bit for bit.
 template <int RPW, int PART, int RPP>
 __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(SolveParams sp, DevBufs d,
                                                                     real update_reg) {
@@ -1206,34 +1213,56 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
       BwsCarry& c = d.carry[rc.b];
       __syncthreads();
-      if (rc.act) {
+      if (rc.live && !rc.failed) {  // (now: a later attempt of another row reuses rl)
         #pragma unroll 1
         for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[(e / 6) * MP + e % 6];
         if (rc.t < 6) c.G[rc.t] = rl.Gs[rc.t];
+      }
+      pending = rc.live && rc.failed;
+      if (pending) {  // the next attempt, as PART 0 would start it
+        rc.reg = fmax(rc.reg * update_reg, real(1e-03));
+        ++bws_iter;
+        if (rc.reg > 1000) {
+          aborted = true;
+          pending = false;
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(pending)) continue;
+      if (rc.act) {
         if (rc.t == 0) {
-          c.ok = rc.failed ? 0 : 1;
+          c.reg = rc.reg;
+          c.abort = aborted ? 1 : 0;
+          c.iter = bws_iter;
+          c.sweeps = (int32_t)sweeps;
           c.knots = (int32_t)rc.kn;
         }
       }
       return;
     }
     if (PART == 2 && first && L.P > L.n_wb) {
-      // resume from the SRB half's value function (or retry if that half failed)
+      // resume the SRB half's passing attempt from its value function (its regularisation,
+      // its attempt number) -- or take over its abort
       const BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       #pragma unroll 1
       for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
       if (rc.lt < 6) rl.Gs[rc.lt] = c.G[rc.lt];
       __syncthreads();
-      rc.failed = rc.live && c.ok == 0;
-      rc.kn += rc.live ? c.knots : 0;
+      if (rc.live) {
+        rc.reg = c.reg;
+        bws_iter = c.iter;
+        sweeps += c.sweeps - 1;
+        rc.kn += c.knots;
+        aborted = c.abort != 0;
+      }
+      rc.failed = rc.live && aborted;
       rc.dV = st->dV[L.n_wb];
       sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
       sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, 0);
     }
-    pending = rc.live && rc.failed;
+    pending = rc.live && rc.failed && !aborted;
     if (pending) {
       rc.reg = fmax(rc.reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
       ++bws_iter;

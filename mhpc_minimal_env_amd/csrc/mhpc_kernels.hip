@@ -1062,8 +1062,9 @@ constexpr int kParGroups = MHPC_PAR_GROUPS;
 constexpr int kParD0[4] = {2, kParGroups == 4 ? 5 : 9, 9, 14};
 constexpr int kParD1[4] = {kParGroups == 4 ? 5 : 7, kParGroups == 4 ? 7 : 18, 14, 18};
 
+// rec: the knot's piece of column block 0 (column c at rec + c * NK * 9, mhpc_solver.h par_col)
 template <int SF, int G>
-__device__ __forceinline__ void partials_knot(const real* nk, real* rec) {
+__device__ __forceinline__ void partials_knot(const real* nk, real* rec, int NK) {
   constexpr int d0 = kParD0[G], d1 = kParD1[G];
   real x[14], u[4];
 #pragma unroll
@@ -1077,21 +1078,21 @@ __device__ __forceinline__ void partials_knot(const real* nk, real* rec) {
     real o[9];
     wb_knot_partial_q<SF>(x, K, dir, o);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+    for (int i = 0; i < 9; ++i) rec[(size_t)dir * NK * 9 + i] = o[i];
   }
 #pragma unroll 1
   for (int dir = d0 > 9 ? d0 : 9; dir < (d1 < 14 ? d1 : 14); ++dir) {
     real o[9];
     wb_knot_partial_qd<SF>(x, K, dir, o);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+    for (int i = 0; i < 9; ++i) rec[(size_t)dir * NK * 9 + i] = o[i];
   }
 #pragma unroll 1
   for (int dir = d0 > 14 ? d0 : 14; dir < d1; ++dir) {
     real o[9];
     wb_knot_partial_u<SF>(K, dir, o);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) rec[dir * 9 + i] = o[i];
+    for (int i = 0; i < 9; ++i) rec[(size_t)dir * NK * 9 + i] = o[i];
   }
 }
 
@@ -1126,10 +1127,10 @@ __global__ __launch_bounds__(MHPC_PAR_BLOCK, MHPC_PAR_MINB) void k_partials(Solv
   const int k = it - L.par_knot_off[p];
   const int ko = L.ko[p], mode = L.mode[p];
   const real* nk = traj_ptr(sp, d, b, st->nom_slot, ko + k);
-  real* rec = d.par + ((size_t)b * sp.NK + ko + k) * PS;
-  if (mode == 1) partials_knot<kBack, G>(nk, rec);
-  else if (mode == 3) partials_knot<kFront, G>(nk, rec);
-  else partials_knot<-1, G>(nk, rec);
+  real* rec = d.par + par_col(sp.NK, b, 0, ko + k);
+  if (mode == 1) partials_knot<kBack, G>(nk, rec, sp.NK);
+  else if (mode == 3) partials_knot<kFront, G>(nk, rec, sp.NK);
+  else partials_knot<-1, G>(nk, rec, sp.NK);
   if (G == 0) {
     // running-cost derivatives of controls and contact forces at the nominal knot
     // (CostBase.cpp:19-34 + ReB barrier, SinglePhase.cpp:219-249 CALC_PARTIALS_ONLY)
@@ -1137,7 +1138,7 @@ __global__ __launch_bounds__(MHPC_PAR_BLOCK, MHPC_PAR_MINB) void k_partials(Solv
     wb_cost_uy_derivs(sp, mode, L.dt[p], nk + 14, nk + 18, st->reb_active != 0, st->delta[p],
                       st->eps_tq[p], st->eps_grf[p], c);
 #pragma unroll
-    for (int i = 0; i < 14; ++i) rec[PS_JAC + i] = c[i];
+    for (int i = 0; i < 14; ++i) d.par[par_jac(sp.NK, b, ko + k) + i] = c[i];
   }
 }
 

@@ -11,11 +11,12 @@
 //   refpos [B][NK]             forward position reference (ReferenceGen.h:94-109); the
 //          rest of the reference is constant per mode and computed in registers.
 //   K      [B][NK][56], du [B][NK][4], G [B][NK][14]   CostToGoStruct outputs per knot.
-//   par    [B][NK][PS]         dynamics Jacobians of the nominal trajectory: 18 tangent
-//          directions x (7 qddot rows + 2 contact-force rows) per WB knot, followed by the
-//          knot's control/force cost derivatives incl. the ReB barrier (computed once per
-//          partials pass, so the backward kernel evaluates no transcendental); SRB knots
-//          are differentiated in registers by the backward kernel.
+//   par    [B][18][NK][9] + [B][NK][14] (NK * PS per problem, par_col / par_jac below)
+//          dynamics Jacobians of the nominal trajectory: 18 tangent directions x (7 qddot
+//          rows + 2 contact-force rows) per WB knot, column-block major, then the knots'
+//          control/force cost derivatives incl. the ReB barrier (computed once per partials
+//          pass, so the backward kernel evaluates no transcendental); SRB knots are
+//          differentiated in registers by the backward kernel.
 //   px     [B][P][196]         impact Jacobian Px (column-major) at the end of WB phases.
 //   state  [B]                 ProbState (control flow + AL/ReB parameters).
 //   lay    [L]                 Layout table (read through the constant address space: scalar
@@ -34,6 +35,16 @@ constexpr int KS = 24;        // doubles per knot record in traj
 constexpr int PS_JAC = 162;   // 18 tangent directions x (7 qddot + 2 contact-force rows)
 constexpr int PS = 176;       // doubles per knot in par: Jacobians + 14 cost derivatives
                               // (lu 4, luu 4, ly 2, lyy 4 of the stance block)
+// par, per problem (NK = the knot stride, sp.NK): 18 column blocks [NK][9] -- column c of
+// knot k at (c NK + k) 9 -- then the cost derivatives [NK][14].  A direction's values of
+// consecutive knots are contiguous, so the partials' lanes (consecutive knots) store whole
+// lines; the sweep's lane walks its own column block backwards, one 72-byte piece per knot.
+__host__ __device__ inline size_t par_col(int NK, int b, int c, int kk) {
+  return (size_t)b * NK * PS + ((size_t)c * NK + kk) * 9;
+}
+__host__ __device__ inline size_t par_jac(int NK, int b, int kk) {
+  return (size_t)b * NK * PS + (size_t)PS_JAC * NK + (size_t)kk * 14;
+}
 constexpr int MAXP = MHPC_MAX_PHASES;
 constexpr int MAXC = 32;      // max line-search candidates
 constexpr int MAXL = MHPC_MAX_LAYOUTS;  // distinct phase layouts per handle
@@ -151,12 +162,15 @@ struct ProbState {
 
 // Value function where the backward sweep crosses from the SRB phases into the WB phases
 // (the sweep runs as two launches when the SRB part overlaps the partials):
-// H / G of knot 0 of phase n_wb (row stride NX of that phase), whether that part of the
-// first sweep attempt passed the PSD test, and the knots it swept.
+// H / G of knot 0 of phase n_wb (row stride NX of that phase) from the first attempt whose
+// SRB part passed the PSD test -- the SRB half retries attempts that fail there itself --,
+// that attempt's regularisation and number (bws_iter), whether the retries aborted
+// (regularisation > 1000), the attempts and SRB knots swept.
 struct BwsCarry {
   real H[196];
   real G[14];
-  int32_t ok, knots;
+  real reg;
+  int32_t abort, iter, sweeps, knots;
 };
 
 struct DevBufs {

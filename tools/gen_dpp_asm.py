@@ -43,12 +43,18 @@ class Block:
     def __init__(self, name, naccs, arrays, terms, doc):
         self.name, self.naccs, self.arrays, self.terms, self.doc = name, naccs, arrays, terms, doc
 
+    @staticmethod
+    def round_terms(rnd):
+        """(accumulator, term) pairs of a round: terms are (src, m, lane) for accumulators
+        0, 1, ... in order, or (acc, src, m, lane) for a sparse round."""
+        return [(t[0], t[1:]) if len(t) == 4 else (a, t) for a, t in enumerate(rnd)]
+
     def emit(self):
         # operand numbering: accumulators, then every array element used (in order of use)
         ops, index = [], {}
         nxt = self.naccs
         for rnd in self.terms:
-            for src, m, _ in rnd:
+            for _, (src, m, _) in self.round_terms(rnd):
                 for e in (src, m):
                     if e not in index:
                         index[e] = nxt
@@ -62,14 +68,18 @@ class Block:
                + ", ".join(f"const T* {n}" for n in self.arrays) + ") {"]
         for t, mn in (("double", "v_fmac_f64_dpp"), ("float", "v_fmac_f32_dpp")):
             lines = ["s_nop 1"]
-            pad = max(0, 3 - self.naccs)
             k = 0
+            last = {}  # accumulator -> issue slot of its last write
             for rnd in self.terms:
-                for a, (src, m, lane) in enumerate(rnd):
-                    if k and pad and k % self.naccs == 0:
-                        lines.append(f"s_nop {pad - 1}")
+                for a, (src, m, lane) in self.round_terms(rnd):
+                    # an accumulator re-read within 2 wait states of its write: pad
+                    gap = k - last[a] - 1 if a in last else 2
+                    if gap < 2:
+                        lines.append(f"s_nop {1 - gap}")
+                        k += 2 - gap
                     lines.append(f"{mn} %{a}, %{index[src]}, %{index[m]} row_newbcast:{lane} "
                                  "row_mask:0xf bank_mask:0xf")
+                    last[a] = k
                     k += 1
             kw = "if constexpr (sizeof(T) == 8)" if t == "double" else "else"
             out.append(f"  {kw}")
@@ -153,10 +163,19 @@ def blocks():
     B.append(Block("wb2_st_b", 7, ["g", "g2", "cc", "cc2"], terms,
                    "two-row stance terms, slots 6..10 and the control rows 2, 3"))
     # ---- SRB (NQ = 3) ----
-    for nm, cols in (("a", range(0, 5)), ("b", range(5, 10))):
-        B.append(col_block(f"srb_s_{nm}", 3, list(cols), 3, ["w", "h"],
-                           lambda c, j: f"w[{j}]", lambda c, j: f"h[{j}]",
-                           f"SRB S = H [A B], columns {cols.start}..{cols.stop - 1}"))
+    # sparse S = H [A B] of the SRB knot: the terms whose W entry is structurally non-zero
+    # (FBDynamics_par.c: row 3 has columns 3, 6, 8; row 4 columns 4, 7, 9; row 5 columns 0, 1,
+    # 5..9), in the dense blocks' order r = 0, 1, 2 -- a skipped term added an exact zero
+    nzr = {0: [2], 1: [2], 2: [], 3: [0], 4: [1], 5: [2], 6: [0, 2], 7: [1, 2], 8: [0, 2], 9: [1, 2]}
+    for nm, cols in (("a", [0, 1, 3, 4]), ("b", [5, 6, 7, 8, 9])):
+        rounds = []
+        for j in range(2):
+            rnd = [(a, f"w[{nzr[c][j]}]", f"h[{nzr[c][j]}]", lam(3, c))
+                   for a, c in enumerate(cols) if j < len(nzr[c])]
+            if rnd:
+                rounds.append(rnd)
+        B.append(Block(f"srb_sp_{nm}", len(cols), ["w", "h"], rounds,
+                       f"SRB S = H [A B], structurally non-zero terms of columns {cols}"))
     B.append(col_block("srb_h", 3, list(range(6)), 4, ["qxu", "k"],
                        lambda c, j: f"qxu[{j}]", lambda c, j: f"k[{j}]", "SRB H update"))
     for c in (5, 6):

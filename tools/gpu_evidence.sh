@@ -19,10 +19,11 @@ run c2_b1 --workload c2
 run c2_b1024 --workload c2 --batch-per-gpu 1024 --no-cpu-baseline
 run c5_b4096 --workload c5 --cpu-sample 2048
 run c5f32_b4096 --workload c5f32 --no-cpu-baseline
+run mixed_b4096 --workload mixed
 timeout -k 10 400 python bench.py --batch-sweep 1,16,64,256,512,1024,2048,4096,8192 --steps 5 --warmup 2 > gpurun_out/sweep_${TAG}.jsonl 2> gpurun_out/sweep_${TAG}.err || { echo "sweep failed"; tail gpurun_out/sweep_${TAG}.err; exit 1; }
 python -c "
 import json
 for l in open('gpurun_out/sweep_${TAG}.jsonl'):
     d = json.loads(l); print('sweep', d['batch'], round(d['value']), 'solves/s', round(d['ms_per_step'], 3), 'ms')
 "
-bash tools/gpu_profile.sh ${TAG}_b1024 1024 && bash tools/gpu_profile.sh ${TAG}_b4096 4096 && WL=c5 bash tools/gpu_profile.sh ${TAG}_c5_b4096 4096 && B=1024 bash tools/gpu_pmc_stalls.sh ${TAG}_sq > gpurun_out/sq_${TAG}.txt 2>&1
+bash tools/gpu_profile.sh ${TAG}_b1024 1024 && bash tools/gpu_profile.sh ${TAG}_b4096 4096 && WL=c5 bash tools/gpu_profile.sh ${TAG}_c5_b4096 4096 && WL=c5f32 bash tools/gpu_profile.sh ${TAG}_c5f32_b4096 4096 && WL=mixed bash tools/gpu_profile.sh ${TAG}_mixed_b4096 4096 && B=1024 bash tools/gpu_pmc_stalls.sh ${TAG}_sq > gpurun_out/sq_${TAG}.txt 2>&1
