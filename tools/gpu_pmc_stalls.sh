@@ -6,7 +6,7 @@ OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --list-avail > $OUT/avail.txt 2>&1 || true
-CMD="python bench.py --steps 1 --warmup 1 --batch-per-gpu ${B:-1024} --no-cpu-baseline"
+CMD="python bench.py --steps 1 --warmup 1 --batch-per-gpu ${B:-1024} --no-cpu-baseline --no-north-star"
 i=0
 for set in "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU" \
            "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM SQ_WAVES" \
