@@ -328,6 +328,17 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       }
 #pragma unroll
       for (int c = 0; c < 14; ++c) pX[c] = nk[c];
+    } else if (PAIR) {  // SRB: the pair splits the four control rows (even u0, u1; odd u2, u3)
+      const int r0 = back ? 2 : 0;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) pK[ii * 6 + c] = Kk[(r0 + ii) * 6 + c];
+        pU[ii] = nk[6 + r0 + ii];
+        pD[ii] = duk[r0 + ii];
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) pX[c] = nk[c];
     } else {
 #pragma unroll
       for (int i = 0; i < 24; ++i) pK[i] = Kk[i];
@@ -383,6 +394,10 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
     const real* Kk = ST ? sgp + 2 * kc * KP : d.K + ((size_t)b * sp.NK + ko + k) * 56;
     const real* duk = ST ? sgp + 2 * (D0 + 2 * kc) : d.du + ((size_t)b * sp.NK + ko + k) * 4;
     if (wb && PAIR) {
+      // the state-only part of the dynamics first: the feedback operands (prefetched from the
+      // LDS stage at the end of the previous knot) land meanwhile
+      WbPairPrep P;
+      wb_pair_prep(x, back, P);
       // the own leg's two torques (rows 2 back, 2 back + 1 of K)
       real u2[2];
       if (PF) {
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         }
       }
       real xd[14], y[4];
-      wb_dynamics_pair(x, u2, mode, back, xd, y);
+      wb_pair_finish(x, u2, mode, back, P, xd, y);
       // ring record split over the pair: x[7 back .. 7 back + 6], own u, own-slot y
 #pragma unroll
       for (int i = 0; i < 7; ++i) rr[i] = back ? x[7 + i] : x[i];
@@ -426,10 +441,23 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       for (int i = 0; i < 14; ++i) x[i] = x[i] + xd[i] * dt;
     } else {
       real u[4];
+      if (PF && PAIR) {  // own two control rows, then the partner's by in-pair broadcasts
+        real uo[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const real fb = PF ? fb_dot<6>(pK + i * 6, x, pX) : fb_dot<6>(Kk + i * 6, x, nk);
-        u[i] = PF ? (pU[i] + eps * pD[i]) + fb : (nk[6 + i] + eps * duk[i]) + fb;
+        for (int ii = 0; ii < 2; ++ii) {
+          const real fb = fb_dot<6>(pK + ii * 6, x, pX);
+          uo[ii] = (pU[ii] + eps * pD[ii]) + fb;
+        }
+        u[0] = pair_from<0>(uo[0]);
+        u[1] = pair_from<0>(uo[1]);
+        u[2] = pair_from<1>(uo[0]);
+        u[3] = pair_from<1>(uo[1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const real fb = PF ? fb_dot<6>(pK + i * 6, x, pX) : fb_dot<6>(Kk + i * 6, x, nk);
+          u[i] = PF ? (pU[i] + eps * pD[i]) + fb : (nk[6 + i] + eps * duk[i]) + fb;
+        }
       }
       real xd[6];
       srb_dynamics(x, u, f, sc, xd);

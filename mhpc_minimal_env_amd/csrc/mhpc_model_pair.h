@@ -205,20 +205,24 @@ MHPC_HD void pair_solve(const PairFactor& F, bool back, const real rb[3],
   xl[1] = w1 - mad(F.Z[1][2], x2, mad(F.Z[1][1], x1, F.Z[1][0] * x0));
 }
 
-template <bool SBACK>
-MHPC_HD void wb_stance_pair(const real* x, const LegGeo<real, real>& L, real sg, real sth,
-                            real cth, bool back, const PairFactor& F, real v[7], real* y);
-
-// x (14, identical on both lanes of the pair), u_own = the own leg's two joint torques.
-// Returns xdot (14) and y (4), identical on both lanes.  mode as wb_dynamics.
-MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
-                                                 bool back, real* xdot, real* y) {
+// What the pair dynamics needs of the state alone (geometry, mass matrix factor, bias): it
+// does not depend on the controls, so the line search evaluates it while the knot's feedback
+// operands are still on their way from LDS (wb_pair_prep, then the feedback, then
+// wb_pair_finish -- the same operations as wb_dynamics_pair, in the same order per value).
+struct WbPairPrep {
+  LegGeo<real, real> L;
+  real sg, sth, cth;
+  real hh, hk;     // own leg joint bias
+  real hb[3];      // base bias
+  PairFactor F;
+};
+MHPC_HD void wb_pair_prep(const real* x, bool back, WbPairPrep& P) {
   MHPC_NO_FMA_WB
   const real sg = back ? -real(1.0) : real(1.0);
   // geometry: the body pitch and the own leg's two links
   const real qh = back ? x[5] : x[3], qk = back ? x[6] : x[4];
   const real qhd = back ? x[12] : x[10], qkd = back ? x[13] : x[11];
-  LegGeo<real, real> L;
+  LegGeo<real, real>& L = P.L;
   const real a1 = x[2] + qh;
   const real a2 = a1 + qk;
   real sv[3], cv[3];
@@ -228,6 +232,7 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   L.s2 = sv[2]; L.c2 = cv[2];
   L.w1 = x[9] + qhd;
   L.w2 = L.w1 + qkd;
+  P.sg = sg; P.sth = sth; P.cth = cth;
   PairLegMH lm;
   pair_leg_mass_bias(L, sg, sth, cth, x[9], lm);
   // base block and base bias: body constant + (front leg + back leg), each leg thigh +
@@ -245,7 +250,7 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   M00 += kShankMass; M11 += kShankMass;
   const real M10 = real(0.0), M20 = bs[0], M21 = bs[1], M22 = bs[2];
   // arrowhead factorisation (arrow_factor), own leg block, Schur terms swapped
-  PairFactor F;
+  PairFactor& F = P.F;
   {
     const real a = lm.Mhh, b = lm.Mkh, c = lm.Mkk;
     const real rdet = pivot_rcp(mad(a, c, -(b * b)));
@@ -282,12 +287,25 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
     F.Si[4] = mad(s20, s10, -(s00 * s21)) * rdet;
     F.Si[5] = mad(s00, s11, -(s10 * s10)) * rdet;
   }
+  P.hh = lm.hh;
+  P.hk = lm.hk;
+  P.hb[0] = bs[3]; P.hb[1] = bs[4]; P.hb[2] = bs[5];
+}
+
+template <bool SBACK>
+MHPC_HD void wb_stance_pair(const real* x, const LegGeo<real, real>& L, real sg, real sth,
+                            real cth, bool back, const PairFactor& F, real v[7], real* y);
+
+// The controls' part: M v = S'u - h, the contact correction, xdot.
+MHPC_HD void wb_pair_finish(const real* x, const real u_own[2], int mode, bool back,
+                            const WbPairPrep& P, real* xdot, real* y) {
+  MHPC_NO_FMA_WB
   // unconstrained accelerations: M v = S'u - h
   real vb[3], vl[2];
   {
-    const real rb[3] = {-bs[3], -bs[4], -bs[5]};
-    const real rl[2] = {u_own[0] - lm.hh, u_own[1] - lm.hk};
-    pair_solve(F, back, rb, rl, vb, vl);
+    const real rb[3] = {-P.hb[0], -P.hb[1], -P.hb[2]};
+    const real rl[2] = {u_own[0] - P.hh, u_own[1] - P.hk};
+    pair_solve(P.F, back, rb, rl, vb, vl);
   }
   // full v in model order (front leg, back leg)
   real v[7];
@@ -296,13 +314,22 @@ MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
   pair_order(back, vl[1], &v[4], &v[6]);
 #pragma unroll
   for (int i = 0; i < 4; ++i) y[i] = real(0.0);
-  if (mode == 1) wb_stance_pair<true>(x, L, sg, sth, cth, back, F, v, y);
-  else if (mode == 3) wb_stance_pair<false>(x, L, sg, sth, cth, back, F, v, y);
+  if (mode == 1) wb_stance_pair<true>(x, P.L, P.sg, P.sth, P.cth, back, P.F, v, y);
+  else if (mode == 3) wb_stance_pair<false>(x, P.L, P.sg, P.sth, P.cth, back, P.F, v, y);
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     xdot[i] = x[7 + i];
     xdot[7 + i] = v[i];
   }
+}
+
+// x (14, identical on both lanes of the pair), u_own = the own leg's two joint torques.
+// Returns xdot (14) and y (4), identical on both lanes.  mode as wb_dynamics.
+MHPC_HD void wb_dynamics_pair(const real* x, const real u_own[2], int mode,
+                                                 bool back, real* xdot, real* y) {
+  WbPairPrep P;
+  wb_pair_prep(x, back, P);
+  wb_pair_finish(x, u_own, mode, back, P, xdot, y);
 }
 
 // The contact KKT correction of a stance mode (kkt_contact), SBACK = the back foot is down
