@@ -240,6 +240,7 @@ struct RowCtx {
   bool act;    // the row holds an active problem in this launch
   bool live;   // the row takes part in the current sweep attempt
   bool failed; // ... and its attempt has failed (PSD test) -- sticky for the attempt
+  bool spec;   // a speculative attempt: computes its value function only, writes no output
   int nom;     // nominal trajectory slot
   real reg;    // regularisation of the attempt
   acc dV;      // expected cost change (row-uniform)
@@ -265,8 +266,15 @@ __device__ __forceinline__ bool any_go(const RowCtx& r) {
 // Per knot the partials record (mhpc_solver.h: 18 columns x (7 qddot rows + 2 force rows),
 // then lu, luu, ly, lyy) is read straight into the lanes that own its columns; the next
 // knot's record is loaded while the current one computes.
+// knot iterations a sweep function ran: only the timing build keeps the count
+#ifdef MHPC_BWS_TIMING
+#define BWS_ITERS(n) (n)
+#else
+#define BWS_ITERS(n) 0
+#endif
+
 template <bool STANCE>
-__device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
+__device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                          RowCtx& rc, int p) {
   using R = Rows<7>;
   using wk = wreal;
@@ -299,13 +307,17 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
   const int cq = t < NCS ? t : 0;
   // (the nominal state first: the wait for the last load of a knot then never covers the
   // stores of the previous knot, which share gfx950's in-order VM counter)
+  // the phase's operand bases (knot 0): a knot adds k times its record stride
+  const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko) + xi;
+  const real* jc0 = d.par + par_jac(sp.NK, b, ko) + cq;
+  const real* r10 = d.par + par_col(sp.NK, b, c1, ko);
+  const real* r20 = d.par + par_col(sp.NK, b, c2, ko);
   auto load = [&](int k) {
-    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
-    pxn = tk[xi];
+    pxn = tk0[k * KS];
     ppos = pos[k];
-    pcv = d.par[par_jac(sp.NK, b, ko + k) + cq];
-    const real* r1 = d.par + par_col(sp.NK, b, c1, ko + k);
-    const real* r2 = d.par + par_col(sp.NK, b, c2, ko + k);
+    pcv = jc0[k * 14];
+    const real* r1 = r10 + k * 9;
+    const real* r2 = r20 + k * 9;
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr1[r] = r1[r];
 #pragma unroll
@@ -325,22 +337,27 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
   // gfx950 counts loads and stores on one in-order VM counter.
   PendingKnot pend;
   pend.ok = false;
+  const size_t rec0 = (size_t)b * sp.NK + ko;
+  real* const K0 = d.K + rec0 * 56 + rho;
+  real* const G0 = d.G + rec0 * 14 + rho;
+  real* const du0 = d.du + rec0 * 4;
   auto store_pending = [&]() {
     if (pend.ok) {
-      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
       if (xl) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = pend.K[a];
-        d.G[rec * 14 + rho] = pend.G;
+        for (int a = 0; a < 4; ++a) K0[pend.k * 56 + a * 14] = pend.K[a];
+        G0[pend.k * 14] = pend.G;
       } else if (t == 14) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+        for (int a = 0; a < 4; ++a) du0[pend.k * 4 + a] = pend.du[a];
       }
     }
     pend.ok = false;
   };
   if (N >= 2) load(N - 2);
+  int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
   for (int k = N - 2; k >= 0; --k) {
+    ++it;
     // ---- the knot's derivatives (prefetched) ----
     real W1[7], W2[7], G2o[2], G22[2];
 #pragma unroll
@@ -495,7 +512,7 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
     // ---- outputs of knot k (only while the row's attempt is alive) ----
     const bool ok = gate && psd;
     // outputs of knot k, stored at the top of the next knot (see store_pending)
-    pend.ok = ok;
+    pend.ok = ok && !rc.spec;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -516,6 +533,7 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
+  return BWS_ITERS(it);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -530,7 +548,7 @@ __device__ void sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& 
 // entry is computed with the one-row sweep's operations in the same order, so the two
 // layouts agree bit for bit (tests/test_gpu_variants.py).
 template <bool STANCE>
-__device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
+__device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<7>;
   using wk = wreal;
@@ -565,14 +583,19 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
   real pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;
   const int c2 = 16 + (t & 1);
   const int cq = t < NCS ? t : 0;
+  // the phase's operand / output bases (knot 0): a knot adds k times its record stride
+  const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko) + xi;
+  const real* jc0 = d.par + par_jac(sp.NK, b, ko) + cq;
+  const real* r10 = d.par + par_col(sp.NK, b, rho, ko);
+  const real* rb0 = d.par + par_col(sp.NK, b, cb, ko);
+  const real* r20 = d.par + par_col(sp.NK, b, c2, ko);
   auto load = [&](int k) {
-    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
-    pxn = tk[xi];
+    pxn = tk0[k * KS];
     ppos = pos[k];
-    pcv = d.par[par_jac(sp.NK, b, ko + k) + cq];
-    const real* r1 = d.par + par_col(sp.NK, b, rho, ko + k);
-    const real* rb = d.par + par_col(sp.NK, b, cb, ko + k);
-    const real* r2 = d.par + par_col(sp.NK, b, c2, ko + k);
+    pcv = jc0[k * 14];
+    const real* r1 = r10 + k * 9;
+    const real* rb = rb0 + k * 9;
+    const real* r2 = r20 + k * 9;
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr1[r] = r1[r];
 #pragma unroll
@@ -592,22 +615,27 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
   const int jr = rp ? 7 : 0;            // first matrix row of the row's H columns
   PendingKnot pend;
   pend.ok = false;
+  const size_t rec0 = (size_t)b * sp.NK + ko;
+  real* const K0 = d.K + rec0 * 56 + rho;
+  real* const G0 = d.G + rec0 * 14 + rho;
+  real* const du0 = d.du + rec0 * 4;
   auto store_pending = [&]() {
     if (pend.ok) {
-      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
       if (xl) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 14 + rho] = pend.K[a];
-        d.G[rec * 14 + rho] = pend.G;
+        for (int a = 0; a < 4; ++a) K0[pend.k * 56 + a * 14] = pend.K[a];
+        G0[pend.k * 14] = pend.G;
       } else if (t == 14) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+        for (int a = 0; a < 4; ++a) du0[pend.k * 4 + a] = pend.du[a];
       }
     }
     pend.ok = false;
   };
   if (N >= 2) load(N - 2);
+  int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
   for (int k = N - 2; k >= 0; --k) {
+    ++it;
     real Wo[7], Wb[7], W2[7], G2o[2], G2b[2], G22[2];
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
@@ -744,7 +772,7 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
     for (int s = 0; s < 7; ++s) row_pair_swap(real(Hn[s]), H[s], H[7 + s]);
     Gv = real(Gn);
     const bool ok = gate && psd;
-    pend.ok = ok && rp == 0;
+    pend.ok = ok && rp == 0 && !rc.spec;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -764,6 +792,7 @@ __device__ void sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout&
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
+  return BWS_ITERS(it);
 }
 
 // SRB Jacobian entry of row 3+r, column col of [A B] (FBDynamics_par.c operation order).
@@ -793,7 +822,7 @@ __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const
 // ---------------------------------------------------------------------------------------
 // SRB phase (NQ = 3): the Jacobians are evaluated in registers (FBDynamics_par.c), the cost
 // derivatives from the nominal knot (CostBase.cpp:19-34).
-__device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
+__device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<3>;
   const int t = rc.t, b = rc.b;
@@ -828,8 +857,9 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
   const real W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   real pxs[2], pus[4], pv, ppos;
+  const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko);  // knot k adds k KS
   auto load = [&](int k) {
-    const real* tk = traj_ptr(sp, d, b, rc.nom, ko + k);
+    const real* tk = tk0 + k * KS;
     ppos = pos[k];
     pv = tk[cj];
     pxs[0] = tk[0]; pxs[1] = tk[1];
@@ -846,22 +876,27 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
   const int cr = rho < 10 ? rho : 0;
   PendingKnot pend;  // outputs stored one knot later (see sweep_wb)
   pend.ok = false;
+  const size_t rec0 = (size_t)b * sp.NK + ko;
+  real* const K0 = d.K + rec0 * 56 + rho;
+  real* const G0 = d.G + rec0 * 14 + rho;
+  real* const du0 = d.du + rec0 * 4;
   auto store_pending = [&]() {
     if (pend.ok) {
-      const size_t rec = (size_t)b * sp.NK + ko + pend.k;
       if (xl) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.K[rec * 56 + a * 6 + rho] = pend.K[a];
-        d.G[rec * 14 + rho] = pend.G;
+        for (int a = 0; a < 4; ++a) K0[pend.k * 56 + a * 6] = pend.K[a];
+        G0[pend.k * 14] = pend.G;
       } else if (t == 6) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) d.du[rec * 4 + a] = pend.du[a];
+        for (int a = 0; a < 4; ++a) du0[pend.k * 4 + a] = pend.du[a];
       }
     }
     pend.ok = false;
   };
   if (N >= 2) load(N - 2);
+  int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
   for (int k = N - 2; k >= 0; --k) {
+    ++it;
     real W[3];
     W[0] = W0c;
     W[1] = W1c;
@@ -942,7 +977,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
     for (int j = 0; j < 6; ++j) H[j] = Hn[j];
     Gv = Gn;
     const bool ok = gate && psd;
-    pend.ok = ok && rc.rp == 0;
+    pend.ok = ok && rc.rp == 0 && !rc.spec;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -962,6 +997,7 @@ __device__ void sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout&
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
+  return BWS_ITERS(it);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1013,7 +1049,7 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const La
       if (al) v += 50 * (s * s / 2 * rl.hx[i] * h + lam * rl.hx[i]);
       const real g = v + rl.Gs[i];
       rl.Gs[i] = g;
-      if (gate) Gout[i] = g;
+      if (gate && !rc.spec) Gout[i] = g;
     }
   }
   __syncthreads();
@@ -1112,7 +1148,7 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
         if (wb) impact_step(sp, d, L, rl, rc, p);
         BWS_ADD(5, clock64() - ti0);
       }
-      if (was_go) rc.dV = st->dV[p + 1];  // dVnext
+      if (was_go && !rc.spec) rc.dV = st->dV[p + 1];  // dVnext (a speculative row keeps its own)
     }
     BWS_T(tt0);
     if (wb) {
@@ -1121,25 +1157,28 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
         BWS_ADD(4, clock64() - tt0);
         BWS_T(tw0);
         const int mode = L.mode[p];
+        int nit;
         if (RPP == 2) {
-          if (mode == 1 || mode == 3) sweep_wb2<true>(sp, d, L, st, rl, rc, p);
-          else sweep_wb2<false>(sp, d, L, st, rl, rc, p);
+          if (mode == 1 || mode == 3) nit = sweep_wb2<true>(sp, d, L, st, rl, rc, p);
+          else nit = sweep_wb2<false>(sp, d, L, st, rl, rc, p);
         } else {
-          if (mode == 1 || mode == 3) sweep_wb<true>(sp, d, L, st, rl, rc, p);
-          else sweep_wb<false>(sp, d, L, st, rl, rc, p);
+          if (mode == 1 || mode == 3) nit = sweep_wb<true>(sp, d, L, st, rl, rc, p);
+          else nit = sweep_wb<false>(sp, d, L, st, rl, rc, p);
         }
         BWS_ADD(0, clock64() - tw0);
-        BWS_ADD(1, L.N[p] - 1);
+        BWS_ADD(1, nit);
+        (void)nit;
       }
     } else {
       terminal_value<6>(sp, d, L, st, rl, rc, p);
       BWS_ADD(4, clock64() - tt0);
       BWS_T(ts0);
-      sweep_srb(sp, d, L, st, rl, rc, p);
+      const int nit = sweep_srb(sp, d, L, st, rl, rc, p);
       BWS_ADD(2, clock64() - ts0);
-      BWS_ADD(3, L.N[p] - 1);
+      BWS_ADD(3, nit);
+      (void)nit;
     }
-    if (was_go && rc.lt == 0) st->dV[p] = rc.dV;
+    if (was_go && rc.lt == 0 && !rc.spec) st->dV[p] = rc.dV;
     if (!any_go(rc)) break;
   }
 }
@@ -1172,10 +1211,23 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
 // which it does not read).
 // PART 2: the WB phases of that attempt, then the same retries as PART 0 (whole sweeps) --
 // the same attempts with the same regularisation, bit for bit.
-template <int RPW, int PART, int RPP>
+//
+// Speculative attempts (sp.spec > 0, launches where attempts failing in a WB phase are
+// likely: the first DDP iteration of an AL iteration after the first, where the regularisation
+// restarts from 0).  PART 1 runs sp.spec more copies of its blocks (blockIdx.y = slot): slot j
+// sweeps the SRB phases of attempt (guessed passing attempt) + j at that attempt's
+// regularisation, writing only its value function at the WB boundary, its dV and whether it
+// passed (carry slot j; no K / du / G, no per-phase dV).  When an attempt of PART 2 fails in a
+// WB phase and the next attempt's SRB part is in a slot, the row resumes that attempt at the
+// WB boundary instead of sweeping its SRB phases again (an attempt whose slot failed there is
+// consumed as the serial sweep would have failed it); when the attempt finally passes, the SRB
+// phases are swept once more with its regularisation for their outputs.  Same attempts, same
+// arithmetic per value as PART 0 -- only the SRB re-sweeps of the retries move off the chain.
+template <int RPW, int PART, int RPP, bool SPEC = false>
 __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(SolveParams sp, DevBufs d,
                                                                     real update_reg) {
   static_assert(RPP == 1 || (RPP == 2 && RPW == 2 && PART != 1), "row layout");
+  static_assert(!SPEC || PART != 0, "speculative attempts: the split sweep only");
   __shared__ BwsLds sh;
   BWS_T(tk0);
   const int row = threadIdx.x >> 4;
@@ -1199,10 +1251,44 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
   rc.reg = st->reg;
   rc.kn = rc.kn_wb = rc.px_reads = 0;
   rc.dV = acc(0.0);
+  rc.spec = false;
   int bws_iter = 1;
   int64_t sweeps = 0;
   bool aborted = false;
   bool pending = rc.act;
+  if (SPEC && PART == 1 && blockIdx.y > 0) {
+    // speculative slot j = blockIdx.y: the SRB part of attempt a0 + j, a0 the guessed passing
+    // attempt of slot 0 (2 when the regularisation starts from 0: the first attempt of such a
+    // DDP iteration fails at the first knot with the reference's weights; 1 otherwise)
+    const int j = blockIdx.y;
+    const int att = (st->reg == real(0.0) ? 2 : 1) + j;
+    bool valid = true;
+    for (int i = 1; i < att; ++i) {
+      rc.reg = fmax(rc.reg * update_reg, real(1e-03));
+      valid = valid && !(rc.reg > 1000);
+    }
+    rc.spec = true;
+    rc.live = rc.act && valid;
+    rc.failed = false;
+    zero_value(rl, rc);
+    if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
+    BwsCarry& c = d.carry[(size_t)rc.b * NCARRY + j];
+    __syncthreads();
+    if (rc.act) {
+      #pragma unroll 1
+      for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[(e / 6) * MP + e % 6];
+      if (rc.t < 6) c.G[rc.t] = rl.Gs[rc.t];
+      if (rc.t == 0) {
+        c.reg = rc.reg;
+        c.dV = rc.dV;
+        c.iter = valid && L.P > L.n_wb ? att : -1;
+        c.ok = rc.failed ? 0 : 1;
+        c.knots = (int32_t)rc.kn;
+      }
+    }
+    return;
+  }
+  bool spec_att = false;  // the row's current attempt resumed from a speculative slot
   for (bool first = true;; first = false) {
     rc.live = pending;
     rc.failed = false;
@@ -1211,7 +1297,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       zero_value(rl, rc);
       // (a layout without SRB phases passes with nothing swept; PART 2 sweeps it whole)
       if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
-      BwsCarry& c = d.carry[rc.b];
+      BwsCarry& c = d.carry[(size_t)rc.b * NCARRY];
       __syncthreads();
       if (rc.live && !rc.failed) {  // (now: a later attempt of another row reuses rl)
         #pragma unroll 1
@@ -1242,7 +1328,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     if (PART == 2 && first && L.P > L.n_wb) {
       // resume the SRB half's passing attempt from its value function (its regularisation,
       // its attempt number) -- or take over its abort
-      const BwsCarry& c = d.carry[rc.b];
+      const BwsCarry& c = d.carry[(size_t)rc.b * NCARRY];
       __syncthreads();
       #pragma unroll 1
       for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
@@ -1257,6 +1343,32 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       }
       rc.failed = rc.live && aborted;
       rc.dV = st->dV[L.n_wb];
+      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
+    } else if (SPEC && PART == 2 && L.P > L.n_wb) {
+      // this attempt's SRB part from a speculative slot, if one holds it
+      int js = 0;
+      if (rc.live)
+        for (int j = 1; j <= sp.spec; ++j)
+          if (d.carry[(size_t)rc.b * NCARRY + j].iter == bws_iter) js = j;
+      const bool sa = js > 0;  // (only live rows: the others keep the flag of their last attempt)
+      if (rc.live) spec_att = sa;
+      // the other rows sweep the attempt's SRB phases
+      const bool live = rc.live;
+      rc.live = live && !sa;
+      zero_value(rl, rc);
+      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
+      rc.live = live;
+      __syncthreads();
+      if (sa) {
+        const BwsCarry& c = d.carry[(size_t)rc.b * NCARRY + js];
+        #pragma unroll 1
+        for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
+        if (rc.lt < 6) rl.Gs[rc.lt] = c.G[rc.lt];
+        if (rc.lt == 0) st->dV[L.n_wb] = c.dV;  // dVnext of the last WB phase
+        rc.failed = c.ok == 0;                  // failed in its SRB part
+        rc.dV = c.dV;
+      }
+      __syncthreads();
       sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
@@ -1273,6 +1385,14 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     }
     if (!__builtin_amdgcn_ballot_w64(pending)) break;
   }
+  if (SPEC && PART == 2 && __builtin_amdgcn_ballot_w64(rc.act && spec_att && !aborted)) {
+    // the passing attempt resumed from a slot: its SRB phases once more, for their outputs
+    // (K, du, G of the SRB knots, the SRB phases' dV) -- the same sweep the slot passed
+    rc.live = rc.act && spec_att && !aborted;
+    rc.failed = false;
+    zero_value(rl, rc);
+    sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
+  }
   BWS_ADD(6, clock64() - tk0);
   BWS_ADD(7, 1);
   if (rc.act && rc.lt == 0) {
@@ -1282,7 +1402,12 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     st->cnt[C_BWS_KNOTS_WB] += rc.kn_wb;
     st->cnt[C_BWS_KNOTS_FB] += rc.kn - rc.kn_wb;
     st->cnt[C_PX_READS] += rc.px_reads;
-    if (PART == 2) st->cnt[C_BWS_KNOTS_FB1] += d.carry[rc.b].knots;
+    if (PART == 2) {  // the SRB half's knots: its chain and the speculative slots
+      int64_t kf = d.carry[(size_t)rc.b * NCARRY].knots;
+      if (SPEC)
+        for (int j = 1; j <= sp.spec; ++j) kf += d.carry[(size_t)rc.b * NCARRY + j].knots;
+      st->cnt[C_BWS_KNOTS_FB1] += kf;
+    }
     st->bws_iter = bws_iter;
     if (aborted) {  // "Regularization term exceeds maximum value": return from solve()
       st->status = MHPC_SOLVE_REG_ABORT;
@@ -1327,15 +1452,21 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
                                                      v == MHPC_VARIANT_BWS_PAIRS2) ? 2 : 4;
   const dim3 grid(bws_grid(sp, rpw));
   const dim3 grid4(bws_grid(sp, 4));
+  // the SRB half: slot 0 (its attempt chain) and sp.spec speculative slots
+  const dim3 gridS(bws_grid(sp, rpw), 1 + sp.spec), gridS4(bws_grid(sp, 4), 1 + sp.spec);
 #define MHPC_LAUNCH_BWS(R)                                                                    \
   do {                                                                                        \
-    if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    if (part == 1 && sp.spec) hipLaunchKernelGGL((k_bws<R, 1, 1, true>), gridS, dim3(64), 0, s, sp, d, update_reg); \
+    else if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    else if (part == 2 && sp.spec) hipLaunchKernelGGL((k_bws<R, 2, 1, true>), grid, dim3(64), 0, s, sp, d, update_reg); \
     else if (part == 2) hipLaunchKernelGGL((k_bws<R, 2, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
     else hipLaunchKernelGGL((k_bws<R, 0, 1>), grid, dim3(64), 0, s, sp, d, update_reg);           \
   } while (0)
   if (v == MHPC_VARIANT_BWS_PAIRS2) {
     // the SRB half keeps one row per problem (its knot is short; four problems per wave)
-    if (part == 1) hipLaunchKernelGGL((k_bws<4, 1, 1>), grid4, dim3(64), 0, s, sp, d, update_reg);
+    if (part == 1 && sp.spec) hipLaunchKernelGGL((k_bws<4, 1, 1, true>), gridS4, dim3(64), 0, s, sp, d, update_reg);
+    else if (part == 1) hipLaunchKernelGGL((k_bws<4, 1, 1>), grid4, dim3(64), 0, s, sp, d, update_reg);
+    else if (part == 2 && sp.spec) hipLaunchKernelGGL((k_bws<2, 2, 2, true>), grid, dim3(64), 0, s, sp, d, update_reg);
     else if (part == 2) hipLaunchKernelGGL((k_bws<2, 2, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
     else hipLaunchKernelGGL((k_bws<2, 0, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
   } else if (rpw == 1) MHPC_LAUNCH_BWS(1);
