@@ -312,13 +312,6 @@ void mhpc_destroy(mhpc_handle* h);
                                          an accepted trial without records is rolled out again
                                          into its slot (same arithmetic, bit for bit);
                                          0 = the default (4) */
-#define MHPC_VARIANT_SPEC 5           /* which: speculative SRB attempts of the split sweep
-                                         (mhpc_bws.hip): the SRB half also sweeps the SRB phases
-                                         of the next attempts, so a retry failing in a WB phase
-                                         resumes at the WB boundary; bit for bit the same */
-#define MHPC_VARIANT_SPEC_OFF 1       /*   never */
-#define MHPC_VARIANT_SPEC_ALWAYS 2    /*   in every sweep (the default: the first DDP iteration
-                                         of every AL iteration after the first) */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

@@ -33,8 +33,6 @@ OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_VARIANT_SUBBATCH = 3
 MHPC_MAX_SUBBATCH = 4
 MHPC_VARIANT_RO_STORE = 4  # line-search trials storing their records (0 = default)
-MHPC_VARIANT_SPEC = 5  # speculative SRB attempts of the split sweep
-SPEC_VARIANTS = {"auto": 0, "off": 1, "always": 2}
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1
 MHPC_SOLVE_NONFINITE = 2

@@ -240,7 +240,6 @@ struct RowCtx {
   bool act;    // the row holds an active problem in this launch
   bool live;   // the row takes part in the current sweep attempt
   bool failed; // ... and its attempt has failed (PSD test) -- sticky for the attempt
-  bool spec;   // a speculative attempt: computes its value function only, writes no output
   int nom;     // nominal trajectory slot
   real reg;    // regularisation of the attempt
   acc dV;      // expected cost change (row-uniform)
@@ -512,7 +511,7 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
     // ---- outputs of knot k (only while the row's attempt is alive) ----
     const bool ok = gate && psd;
     // outputs of knot k, stored at the top of the next knot (see store_pending)
-    pend.ok = ok && !rc.spec;
+    pend.ok = ok;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -772,7 +771,7 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
     for (int s = 0; s < 7; ++s) row_pair_swap(real(Hn[s]), H[s], H[7 + s]);
     Gv = real(Gn);
     const bool ok = gate && psd;
-    pend.ok = ok && rp == 0 && !rc.spec;
+    pend.ok = ok && rp == 0;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -977,7 +976,7 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     for (int j = 0; j < 6; ++j) H[j] = Hn[j];
     Gv = Gn;
     const bool ok = gate && psd;
-    pend.ok = ok && rc.rp == 0 && !rc.spec;
+    pend.ok = ok && rc.rp == 0;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -1049,7 +1048,7 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const La
       if (al) v += 50 * (s * s / 2 * rl.hx[i] * h + lam * rl.hx[i]);
       const real g = v + rl.Gs[i];
       rl.Gs[i] = g;
-      if (gate && !rc.spec) Gout[i] = g;
+      if (gate) Gout[i] = g;
     }
   }
   __syncthreads();
@@ -1148,7 +1147,7 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
         if (wb) impact_step(sp, d, L, rl, rc, p);
         BWS_ADD(5, clock64() - ti0);
       }
-      if (was_go && !rc.spec) rc.dV = st->dV[p + 1];  // dVnext (a speculative row keeps its own)
+      if (was_go) rc.dV = st->dV[p + 1];  // dVnext
     }
     BWS_T(tt0);
     if (wb) {
@@ -1178,7 +1177,7 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
       BWS_ADD(3, nit);
       (void)nit;
     }
-    if (was_go && rc.lt == 0 && !rc.spec) st->dV[p] = rc.dV;
+    if (was_go && rc.lt == 0) st->dV[p] = rc.dV;
     if (!any_go(rc)) break;
   }
 }
@@ -1211,23 +1210,10 @@ __device__ void zero_value(RowLds& rl, RowCtx& rc) {
 // which it does not read).
 // PART 2: the WB phases of that attempt, then the same retries as PART 0 (whole sweeps) --
 // the same attempts with the same regularisation, bit for bit.
-//
-// Speculative attempts (sp.spec > 0, launches where attempts failing in a WB phase are
-// likely: the first DDP iteration of an AL iteration after the first, where the regularisation
-// restarts from 0).  PART 1 runs sp.spec more copies of its blocks (blockIdx.y = slot): slot j
-// sweeps the SRB phases of attempt (guessed passing attempt) + j at that attempt's
-// regularisation, writing only its value function at the WB boundary, its dV and whether it
-// passed (carry slot j; no K / du / G, no per-phase dV).  When an attempt of PART 2 fails in a
-// WB phase and the next attempt's SRB part is in a slot, the row resumes that attempt at the
-// WB boundary instead of sweeping its SRB phases again (an attempt whose slot failed there is
-// consumed as the serial sweep would have failed it); when the attempt finally passes, the SRB
-// phases are swept once more with its regularisation for their outputs.  Same attempts, same
-// arithmetic per value as PART 0 -- only the SRB re-sweeps of the retries move off the chain.
-template <int RPW, int PART, int RPP, bool SPEC = false>
+template <int RPW, int PART, int RPP>
 __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(SolveParams sp, DevBufs d,
                                                                     real update_reg) {
   static_assert(RPP == 1 || (RPP == 2 && RPW == 2 && PART != 1), "row layout");
-  static_assert(!SPEC || PART != 0, "speculative attempts: the split sweep only");
   __shared__ BwsLds sh;
   BWS_T(tk0);
   const int row = threadIdx.x >> 4;
@@ -1251,44 +1237,10 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
   rc.reg = st->reg;
   rc.kn = rc.kn_wb = rc.px_reads = 0;
   rc.dV = acc(0.0);
-  rc.spec = false;
   int bws_iter = 1;
   int64_t sweeps = 0;
   bool aborted = false;
   bool pending = rc.act;
-  if (SPEC && PART == 1 && blockIdx.y > 0) {
-    // speculative slot j = blockIdx.y: the SRB part of attempt a0 + j, a0 the guessed passing
-    // attempt of slot 0 (2 when the regularisation starts from 0: the first attempt of such a
-    // DDP iteration fails at the first knot with the reference's weights; 1 otherwise)
-    const int j = blockIdx.y;
-    const int att = (st->reg == real(0.0) ? 2 : 1) + j;
-    bool valid = true;
-    for (int i = 1; i < att; ++i) {
-      rc.reg = fmax(rc.reg * update_reg, real(1e-03));
-      valid = valid && !(rc.reg > 1000);
-    }
-    rc.spec = true;
-    rc.live = rc.act && valid;
-    rc.failed = false;
-    zero_value(rl, rc);
-    if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
-    BwsCarry& c = d.carry[(size_t)rc.b * NCARRY + j];
-    __syncthreads();
-    if (rc.act) {
-      #pragma unroll 1
-      for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[(e / 6) * MP + e % 6];
-      if (rc.t < 6) c.G[rc.t] = rl.Gs[rc.t];
-      if (rc.t == 0) {
-        c.reg = rc.reg;
-        c.dV = rc.dV;
-        c.iter = valid && L.P > L.n_wb ? att : -1;
-        c.ok = rc.failed ? 0 : 1;
-        c.knots = (int32_t)rc.kn;
-      }
-    }
-    return;
-  }
-  bool spec_att = false;  // the row's current attempt resumed from a speculative slot
   for (bool first = true;; first = false) {
     rc.live = pending;
     rc.failed = false;
@@ -1297,7 +1249,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       zero_value(rl, rc);
       // (a layout without SRB phases passes with nothing swept; PART 2 sweeps it whole)
       if (L.P > L.n_wb) sweep_phases<false, 1>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
-      BwsCarry& c = d.carry[(size_t)rc.b * NCARRY];
+      BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       if (rc.live && !rc.failed) {  // (now: a later attempt of another row reuses rl)
         #pragma unroll 1
@@ -1328,7 +1280,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     if (PART == 2 && first && L.P > L.n_wb) {
       // resume the SRB half's passing attempt from its value function (its regularisation,
       // its attempt number) -- or take over its abort
-      const BwsCarry& c = d.carry[(size_t)rc.b * NCARRY];
+      const BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       #pragma unroll 1
       for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
@@ -1343,32 +1295,6 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       }
       rc.failed = rc.live && aborted;
       rc.dV = st->dV[L.n_wb];
-      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
-    } else if (SPEC && PART == 2 && L.P > L.n_wb) {
-      // this attempt's SRB part from a speculative slot, if one holds it
-      int js = 0;
-      if (rc.live)
-        for (int j = 1; j <= sp.spec; ++j)
-          if (d.carry[(size_t)rc.b * NCARRY + j].iter == bws_iter) js = j;
-      const bool sa = js > 0;  // (only live rows: the others keep the flag of their last attempt)
-      if (rc.live) spec_att = sa;
-      // the other rows sweep the attempt's SRB phases
-      const bool live = rc.live;
-      rc.live = live && !sa;
-      zero_value(rl, rc);
-      sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
-      rc.live = live;
-      __syncthreads();
-      if (sa) {
-        const BwsCarry& c = d.carry[(size_t)rc.b * NCARRY + js];
-        #pragma unroll 1
-        for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
-        if (rc.lt < 6) rl.Gs[rc.lt] = c.G[rc.lt];
-        if (rc.lt == 0) st->dV[L.n_wb] = c.dV;  // dVnext of the last WB phase
-        rc.failed = c.ok == 0;                  // failed in its SRB part
-        rc.dV = c.dV;
-      }
-      __syncthreads();
       sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.n_wb - 1, 0);
     } else {
       zero_value(rl, rc);
@@ -1385,14 +1311,6 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     }
     if (!__builtin_amdgcn_ballot_w64(pending)) break;
   }
-  if (SPEC && PART == 2 && __builtin_amdgcn_ballot_w64(rc.act && spec_att && !aborted)) {
-    // the passing attempt resumed from a slot: its SRB phases once more, for their outputs
-    // (K, du, G of the SRB knots, the SRB phases' dV) -- the same sweep the slot passed
-    rc.live = rc.act && spec_att && !aborted;
-    rc.failed = false;
-    zero_value(rl, rc);
-    sweep_phases<true, RPP>(sp, d, L, st, rl, rc, L.P - 1, L.n_wb);
-  }
   BWS_ADD(6, clock64() - tk0);
   BWS_ADD(7, 1);
   if (rc.act && rc.lt == 0) {
@@ -1402,12 +1320,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     st->cnt[C_BWS_KNOTS_WB] += rc.kn_wb;
     st->cnt[C_BWS_KNOTS_FB] += rc.kn - rc.kn_wb;
     st->cnt[C_PX_READS] += rc.px_reads;
-    if (PART == 2) {  // the SRB half's knots: its chain and the speculative slots
-      int64_t kf = d.carry[(size_t)rc.b * NCARRY].knots;
-      if (SPEC)
-        for (int j = 1; j <= sp.spec; ++j) kf += d.carry[(size_t)rc.b * NCARRY + j].knots;
-      st->cnt[C_BWS_KNOTS_FB1] += kf;
-    }
+    if (PART == 2) st->cnt[C_BWS_KNOTS_FB1] += d.carry[rc.b].knots;
     st->bws_iter = bws_iter;
     if (aborted) {  // "Regularization term exceeds maximum value": return from solve()
       st->status = MHPC_SOLVE_REG_ABORT;
@@ -1452,21 +1365,15 @@ hipError_t launch_bws(const SolveParams& sp, const DevBufs& d, real update_reg, 
                                                      v == MHPC_VARIANT_BWS_PAIRS2) ? 2 : 4;
   const dim3 grid(bws_grid(sp, rpw));
   const dim3 grid4(bws_grid(sp, 4));
-  // the SRB half: slot 0 (its attempt chain) and sp.spec speculative slots
-  const dim3 gridS(bws_grid(sp, rpw), 1 + sp.spec), gridS4(bws_grid(sp, 4), 1 + sp.spec);
 #define MHPC_LAUNCH_BWS(R)                                                                    \
   do {                                                                                        \
-    if (part == 1 && sp.spec) hipLaunchKernelGGL((k_bws<R, 1, 1, true>), gridS, dim3(64), 0, s, sp, d, update_reg); \
-    else if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
-    else if (part == 2 && sp.spec) hipLaunchKernelGGL((k_bws<R, 2, 1, true>), grid, dim3(64), 0, s, sp, d, update_reg); \
+    if (part == 1) hipLaunchKernelGGL((k_bws<R, 1, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
     else if (part == 2) hipLaunchKernelGGL((k_bws<R, 2, 1>), grid, dim3(64), 0, s, sp, d, update_reg); \
     else hipLaunchKernelGGL((k_bws<R, 0, 1>), grid, dim3(64), 0, s, sp, d, update_reg);           \
   } while (0)
   if (v == MHPC_VARIANT_BWS_PAIRS2) {
     // the SRB half keeps one row per problem (its knot is short; four problems per wave)
-    if (part == 1 && sp.spec) hipLaunchKernelGGL((k_bws<4, 1, 1, true>), gridS4, dim3(64), 0, s, sp, d, update_reg);
-    else if (part == 1) hipLaunchKernelGGL((k_bws<4, 1, 1>), grid4, dim3(64), 0, s, sp, d, update_reg);
-    else if (part == 2 && sp.spec) hipLaunchKernelGGL((k_bws<2, 2, 2, true>), grid, dim3(64), 0, s, sp, d, update_reg);
+    if (part == 1) hipLaunchKernelGGL((k_bws<4, 1, 1>), grid4, dim3(64), 0, s, sp, d, update_reg);
     else if (part == 2) hipLaunchKernelGGL((k_bws<2, 2, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
     else hipLaunchKernelGGL((k_bws<2, 0, 2>), grid, dim3(64), 0, s, sp, d, update_reg);
   } else if (rpw == 1) MHPC_LAUNCH_BWS(1);

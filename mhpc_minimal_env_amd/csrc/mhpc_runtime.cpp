@@ -546,7 +546,7 @@ int api_create(const mhpc_problem_desc* desc, const mhpc_hsddp_option* opt, int 
   alloc((void**)&d.px, B * MAXP * 196 * sizeof(real));
   alloc((void**)&d.x0, B * 14 * sizeof(real));
   alloc((void**)&d.st, B * sizeof(ProbState));
-  alloc((void**)&d.carry, B * NCARRY * sizeof(BwsCarry));
+  alloc((void**)&d.carry, B * sizeof(BwsCarry));
   alloc((void**)&h->dcnt, MAXL * NCNT * sizeof(unsigned long long));
   alloc((void**)&h->dlay, MAXL * sizeof(Layout));
   alloc((void**)&h->dgidx, B * sizeof(int));
@@ -730,7 +730,7 @@ static DevBufs block_bufs(const DevBufs& d, const SolveParams& sp, size_t b0) {
   o.x0 += b0 * 14;
   o.st += b0;
   o.out += b0 * NK * KS;
-  o.carry += b0 * NCARRY;
+  o.carry += b0;
   return o;
 }
 
@@ -785,18 +785,9 @@ static int issue_op(Handle* h, const SolveBlock& k, const SolveOp& op) {
         LAUNCH_ON(h, K_BWS, k.s1, launch_bws(sp, d, ureg, 0, k.s1));
         break;
       }
-      {
-        // speculative SRB attempts where attempts failing in a WB phase are likely: the first
-        // DDP iteration of an AL iteration after the first (its regularisation restarts from
-        // 0; C5: 2-6 attempts per problem, the later ones failing a few dozen knots into the
-        // WB phases)
-        SolveParams sx = sp;
-        const bool likely = op.ddp == 1 && op.al >= 2;
-        sx.spec = sp.var_spec == 1 ? 0 : (sp.var_spec == 2 || likely) ? NSPEC : 0;
-        LAUNCH_ON(h, K_BWS_SRB, k.s1, launch_bws(sx, d, ureg, 1, k.s1));
-        HIPCHK(hipStreamWaitEvent(k.s1, k.join, 0));
-        LAUNCH_ON(h, K_BWS, k.s1, launch_bws(sx, d, ureg, 2, k.s1));
-      }
+      LAUNCH_ON(h, K_BWS_SRB, k.s1, launch_bws(sp, d, ureg, 1, k.s1));
+      HIPCHK(hipStreamWaitEvent(k.s1, k.join, 0));
+      LAUNCH_ON(h, K_BWS, k.s1, launch_bws(sp, d, ureg, 2, k.s1));
       break;
     case OP_LS:
       LAUNCH_ON(h, K_LS, k.s1, launch_rollout(sp, d, op.al, op.ddp, op.max_ddp, 0, k.s1));
@@ -1372,11 +1363,6 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
   if (which == MHPC_VARIANT_OVERLAP) {
     if (variant < 0 || variant > MHPC_VARIANT_OVERLAP_OFF) return fail(MHPC_ERR_INVALID, "no such overlap variant");
     sp.var_overlap = variant;
-    return MHPC_OK;
-  }
-  if (which == MHPC_VARIANT_SPEC) {
-    if (variant < 0 || variant > MHPC_VARIANT_SPEC_ALWAYS) return fail(MHPC_ERR_INVALID, "no such speculation variant");
-    sp.var_spec = variant;
     return MHPC_OK;
   }
   if (which == MHPC_VARIANT_RO_STORE) {

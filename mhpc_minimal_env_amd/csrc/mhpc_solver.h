@@ -101,10 +101,6 @@ struct SolveParams {
   // launch shape (host side only): compute units of the handle's device and the kernel
   // variants forced through mhpc_set_kernel_variant (0 = chosen by batch size)
   int ncu, var_bws, var_ro, var_overlap;
-  // speculative SRB attempts of a split sweep (mhpc_bws.hip k_bws): slots of this launch
-  // (0..NSPEC, set per launch) and the handle's policy (MHPC_VARIANT_SPEC: 0 auto, 1 off,
-  // 2 in every sweep)
-  int spec, var_spec;
   // line-search trials that store their running knot records (the first ro_store, and the
   // last; the rest are rolled out again when accepted -- mhpc_kernels.hip RO_STORE_FIRST)
   int ro_store;
@@ -170,17 +166,11 @@ struct ProbState {
 // SRB part passed the PSD test -- the SRB half retries attempts that fail there itself --,
 // that attempt's regularisation and number (bws_iter), whether the retries aborted
 // (regularisation > 1000), the attempts and SRB knots swept.
-// Slot 0 of a problem's carries is that chain; slots 1..NSPEC hold speculative attempts (the
-// SRB half's extra rows, launched where failures in the WB phases are likely): the SRB part of
-// attempt `iter` at its regularisation, `ok` whether it passed, its dV at the boundary.
-constexpr int NSPEC = 2;
-constexpr int NCARRY = 1 + NSPEC;
 struct BwsCarry {
   real H[196];
   real G[14];
   real reg;
-  acc dV;
-  int32_t abort, iter, sweeps, knots, ok;
+  int32_t abort, iter, sweeps, knots;
 };
 
 struct DevBufs {
@@ -194,7 +184,7 @@ struct DevBufs {
   real* x0;
   ProbState* st;
   real* out;    // export staging [B][NK][KS]
-  BwsCarry* carry;  // [B][NCARRY]
+  BwsCarry* carry;  // [B]
   const Layout* lay;  // [ngrp] layout table
   const int* gidx;    // [B] problems grouped by layout
   const int* lid;     // [B] layout of each problem

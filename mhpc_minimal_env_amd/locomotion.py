@@ -511,18 +511,13 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
     def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto",
-                           sub_batches: int = 0, ro_store: int = 0, spec: str = "auto"):
+                           sub_batches: int = 0, ro_store: int = 0):
         """Pin the backward-sweep / line-search launch variant, the partials / sweep
-        overlap, the number of concurrently scheduled sub-batches, the number of
-        line-search trials that store their knot records and the speculative SRB attempts
-        of the split sweep (mhpc_set_kernel_variant); names in capi.BWS_VARIANTS /
-        capi.RO_VARIANTS / capi.OVERLAP_VARIANTS / capi.SPEC_VARIANTS, "auto" / 0 = chosen by
+        overlap, the number of concurrently scheduled sub-batches and the number of
+        line-search trials that store their knot records (mhpc_set_kernel_variant); names in
+        capi.BWS_VARIANTS / capi.RO_VARIANTS / capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by
         batch size and phase layout (ro_store 0: the default)."""
         L = capi.lib()
-        if spec != "auto" or getattr(self, "_spec_pinned", False):
-            capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SPEC,
-                                                 capi.SPEC_VARIANTS[spec]), "mhpc_set_kernel_variant")
-            self._spec_pinned = spec != "auto"
         if ro_store or getattr(self, "_ro_store_pinned", False):
             capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO_STORE, int(ro_store)),
                        "mhpc_set_kernel_variant")

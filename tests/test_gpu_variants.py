@@ -30,20 +30,18 @@ def _oracle():
 
 
 def solve(desc, x0, bws="auto", rollout="auto", rows=None, overlap="auto", sub_batches=0,
-          ro_store=0, spec="auto", counters=False):
+          ro_store=0):
     from mhpc_minimal_env_amd import locomotion as L
     loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=x0.shape[0], device=0)
     try:
         loco.set_kernel_variant(bws=bws, rollout=rollout, overlap=overlap, sub_batches=sub_batches,
-                                ro_store=ro_store, spec=spec)
+                                ro_store=ro_store)
         loco.set_initial_condition(x0)
         loco.initialization()
         status = loco.solve_mhpc().copy()
         out = loco.concatenated()
         out.update(loco.get_scalars())
         out["status"] = status
-        if counters:
-            out["counters"] = loco.get_counters()
     finally:
         loco.close()
     if rows is not None:
@@ -248,26 +246,3 @@ def test_batch_4096_matches_batch_8_and_oracle(need_gpu, name, precision):
         print(f"fp32 batch-{B} sample: traces {same.sum()}/{len(same)}, J rel err median "
               f"{np.median(rel):.2e} max {rel.max():.2e} (same-trace max {rel[same].max():.2e})")
         assert same.mean() >= FP32_TRACE_MIN_SAMPLE and rel[same].max() <= FP32_J_TOL
-
-
-@pytest.mark.parametrize("wl", ["c5-64", "c5-32", "c3-64"])
-def test_speculative_srb_attempts_bitwise(need_gpu, wl):
-    """Speculative SRB attempts of the split sweep (mhpc_bws.hip k_bws SPEC, MHPC_VARIANT_SPEC):
-    the SRB half also sweeps the SRB phases of the next attempts, so a retry failing in a WB
-    phase resumes at the WB boundary, and the passing attempt's SRB outputs are swept again.
-    Off, in every sweep, and the default (AL iterations after the first) give the same results
-    and decision traces bit for bit -- C5 (whose AL-2 iterations retry up to six times, the
-    later attempts failing in a WB phase), fp64 and fp32, and C3; also with two sub-batches
-    and the two-row / one-row sweep layouts."""
-    from mhpc_minimal_env_amd import configs
-    name, prec = wl.split("-")
-    desc = configs.c5_desc(int(prec)) if name == "c5" else configs.c3_desc()
-    x0 = configs.x0_for(desc, 64)
-    base = solve(desc, x0, spec="off", counters=True)
-    for kw in ({"spec": "always"}, {"spec": "auto"}, {"spec": "always", "sub_batches": 2},
-               {"spec": "always", "bws": "rows4"}, {"spec": "always", "bws": "pairs2"}):
-        got = solve(desc, x0, counters=True, **kw)
-        assert_bitwise(got, base, f"{wl} {kw}")
-    if name == "c5":  # the retries the speculation is for did happen
-        t = np.asarray(base["trace"])
-        assert (t[t >= 0] & 0xFF).max() >= 3
