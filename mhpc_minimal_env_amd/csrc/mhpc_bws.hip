@@ -818,9 +818,48 @@ __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const
   return bc * dt;
 }
 
+// Row 5 (theta) of W, column col, from the lane's two knot operands (srb_w_entry(2, ...) term
+// for term): e0, e1 = u1, u3 (col 0) / u0, u2 (col 1); e0 = z (cols 6, 8) / x (cols 7, 9).
+__device__ __forceinline__ real srb_w2_lane(int col, real e0, real e1, const real* p, const real* s,
+                                            real dt) {
+  MHPC_NO_FMA
+  // every candidate term, then selects (no divergent branches in the knot loop)
+  const int c = col - 6;
+  // (values first, then selects: a select between addresses of the caller's array would
+  // keep that array in scratch)
+  const real f0 = p[0], f1 = p[1], f2 = p[2], f3 = p[3], s0 = s[0], s1 = s[1];
+  real pp = f2;
+  pp = c == 2 ? f3 : pp;
+  pp = c == 1 ? f0 : pp;
+  pp = c == 0 ? f1 : pp;
+  const real bs = (c < 2 ? s0 : s1) * (kSrbInvInertia * (pp - e0));
+  const real ia = s0 * (kSrbInvInertia * e0) + s1 * (kSrbInvInertia * e1);
+  const real ac = col == 0 ? ia : col == 1 ? -ia : real(0.0);
+  const real bc = (c & 1) ? -bs : bs;
+  return col < 6 ? (col == 5 ? real(1.0) : real(0.0)) + ac * dt : bc * dt;
+}
+// Knot-record offsets of a lane's two W-row-5 operands (see srb_w2_lane)
+__device__ __forceinline__ int srb_w2_off(int col, int which) {
+  if (col == 0) return which ? 9 : 7;  // u3 : u1
+  if (col == 1) return which ? 8 : 6;  // u2 : u0
+  if (which == 0 && col >= 6) return (col & 1) ? 0 : 1;  // x (cols 7, 9) : z (cols 6, 8)
+  return 0;  // unused
+}
+
+// Operand prefetch distance of the SRB half's sweep in knots (1: the next knot's operands load
+// while the current one computes; 2: two knots ahead, in two alternating register sets).  2
+// measured -4 % per SRB-half launch at batch 1024 and -13 % at 4096 (beside the partials, whose
+// traffic lengthens the loads' round trips) but does not fit the half's 256-VGPR budget (a few
+// loop-invariant values go to scratch, which the build gate refuses), so 1
+#ifndef MHPC_BWS_SRB_PF
+#define MHPC_BWS_SRB_PF 1
+#endif
+constexpr int SRB_PF_HALF = MHPC_BWS_SRB_PF;
+
 // ---------------------------------------------------------------------------------------
 // SRB phase (NQ = 3): the Jacobians are evaluated in registers (FBDynamics_par.c), the cost
 // derivatives from the nominal knot (CostBase.cpp:19-34).
+template <int SRB_PF>
 __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<3>;
@@ -855,15 +894,19 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
   const real W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
   const real W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
-  real pxs[2], pus[4], pv, ppos;
+  // a lane's knot operands from the nominal: its two W-row-5 operands, its own entry, the
+  // position reference
+  struct Ops {
+    real e0, e1, v, pos;
+  };
   const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko);  // knot k adds k KS
-  auto load = [&](int k) {
+  const int oe0 = srb_w2_off(cj, 0), oe1 = srb_w2_off(cj, 1);
+  auto load = [&](int k, Ops& o) __attribute__((always_inline)) {
     const real* tk = tk0 + k * KS;
-    ppos = pos[k];
-    pv = tk[cj];
-    pxs[0] = tk[0]; pxs[1] = tk[1];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) pus[c] = tk[6 + c];
+    o.pos = pos[k];
+    o.v = tk[cj];
+    o.e0 = tk[oe0];
+    o.e1 = tk[oe1];
   };
   real H[6], Gv;
   {
@@ -892,21 +935,28 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     }
     pend.ok = false;
   };
-  if (N >= 2) load(N - 2);
+  Ops oa, ob;
+  if (N >= 2) load(N - 2, oa);
+  if (SRB_PF > 1 && N >= 3) load(N - 3, ob);
   int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
-  for (int k = N - 2; k >= 0; --k) {
+  // knot k from operand set o; refills o with the operands of knot k - SRB_PF.  False: no row
+  // of the wave goes on
+  auto knot = [&](int k, Ops& o) __attribute__((always_inline)) {
     ++it;
     real W[3];
     W[0] = W0c;
     W[1] = W1c;
-    W[2] = srb_w_entry(2, cj, pxs, pus, foot, cs, dt);
-    const real rxi = rho == 0 ? ppos : rxc;
-    const real l1 = w2 * (pv - rxi);
+    W[2] = srb_w2_lane(cj, o.e0, o.e1, foot, cs, dt);
+    const real rxi = rho == 0 ? o.pos : rxc;
+    const real l1 = w2 * (o.v - rxi);
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     asm volatile("" ::"v"(W[2]), "v"(l1));  // see sweep_wb
+    // (distance 2: issued ahead of the knot's stores, so that the wait for it -- gfx950's single
+    // in-order VM counter -- covers no store of the knot before its use)
+    if (SRB_PF > 1 && k >= SRB_PF) load(k - SRB_PF, o);
     store_pending();
-    if (k > 0) load(k - 1);
+    if (SRB_PF == 1 && k > 0) load(k - 1, o);
     real S[10];
 #pragma unroll
     for (int c = 0; c < 3; ++c) S[c] = H[c];
@@ -986,7 +1036,17 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     pend.G = Gn;
     if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
-    if (!any_go(rc)) break;
+    return any_go(rc);
+  };
+  if (SRB_PF == 1) {
+    for (int k = N - 2; k >= 0; --k)
+      if (!knot(k, oa)) break;
+  } else {
+    // sets alternate (no register copies: a copy would wait for the load on the spot)
+    for (int k = N - 2; k >= 0; k -= 2) {
+      if (!knot(k, oa) || k == 0) break;
+      if (!knot(k - 1, ob)) break;
+    }
   }
   store_pending();
   __syncthreads();
@@ -1172,7 +1232,8 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
       terminal_value<6>(sp, d, L, st, rl, rc, p);
       BWS_ADD(4, clock64() - tt0);
       BWS_T(ts0);
-      const int nit = sweep_srb(sp, d, L, st, rl, rc, p);
+      // (the whole-sweep kernels keep distance 1: their registers go to the WB knots)
+      const int nit = sweep_srb<WB_CODE ? 1 : SRB_PF_HALF>(sp, d, L, st, rl, rc, p);
       BWS_ADD(2, clock64() - ts0);
       BWS_ADD(3, nit);
       (void)nit;
