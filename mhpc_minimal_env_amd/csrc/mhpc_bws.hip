@@ -859,7 +859,9 @@ constexpr int SRB_PF_HALF = MHPC_BWS_SRB_PF;
 // ---------------------------------------------------------------------------------------
 // SRB phase (NQ = 3): the Jacobians are evaluated in registers (FBDynamics_par.c), the cost
 // derivatives from the nominal knot (CostBase.cpp:19-34).
-template <int SRB_PF>
+// LANE_OPS: each lane loads only its row-5 operands (srb_w2_lane); otherwise x, z and u (the
+// whole-sweep kernels: their register allocation is the WB knots', measured slower with it)
+template <int SRB_PF, bool LANE_OPS>
 __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& L, const ProbState* st, RowLds& rl,
                           RowCtx& rc, int p) {
   using R = Rows<3>;
@@ -894,10 +896,10 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
   const real W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
   const real W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
-  // a lane's knot operands from the nominal: its two W-row-5 operands, its own entry, the
-  // position reference
+  // a lane's knot operands from the nominal: its two W-row-5 operands (or x, z, u), its own
+  // entry, the position reference
   struct Ops {
-    real e0, e1, v, pos;
+    real e0, e1, v, pos, xs[2], us[4];
   };
   const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko);  // knot k adds k KS
   const int oe0 = srb_w2_off(cj, 0), oe1 = srb_w2_off(cj, 1);
@@ -905,8 +907,14 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     const real* tk = tk0 + k * KS;
     o.pos = pos[k];
     o.v = tk[cj];
-    o.e0 = tk[oe0];
-    o.e1 = tk[oe1];
+    if (LANE_OPS) {
+      o.e0 = tk[oe0];
+      o.e1 = tk[oe1];
+    } else {
+      o.xs[0] = tk[0]; o.xs[1] = tk[1];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o.us[c] = tk[6 + c];
+    }
   };
   real H[6], Gv;
   {
@@ -946,7 +954,8 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     real W[3];
     W[0] = W0c;
     W[1] = W1c;
-    W[2] = srb_w2_lane(cj, o.e0, o.e1, foot, cs, dt);
+    W[2] = LANE_OPS ? srb_w2_lane(cj, o.e0, o.e1, foot, cs, dt)
+                    : srb_w_entry(2, cj, o.xs, o.us, foot, cs, dt);
     const real rxi = rho == 0 ? o.pos : rxc;
     const real l1 = w2 * (o.v - rxi);
     const bool gate = go(rc);
@@ -1232,8 +1241,9 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
       terminal_value<6>(sp, d, L, st, rl, rc, p);
       BWS_ADD(4, clock64() - tt0);
       BWS_T(ts0);
-      // (the whole-sweep kernels keep distance 1: their registers go to the WB knots)
-      const int nit = sweep_srb<WB_CODE ? 1 : SRB_PF_HALF>(sp, d, L, st, rl, rc, p);
+      // (the whole-sweep kernels keep distance 1 and x, z, u operands: their registers go to
+      // the WB knots)
+      const int nit = sweep_srb<WB_CODE ? 1 : SRB_PF_HALF, !WB_CODE>(sp, d, L, st, rl, rc, p);
       BWS_ADD(2, clock64() - ts0);
       BWS_ADD(3, nit);
       (void)nit;
