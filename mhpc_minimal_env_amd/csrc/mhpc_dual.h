@@ -119,28 +119,36 @@ MHPC_HD real val(Dual a) { return a.v; }
 MHPC_HD real tangent(real) { return real(0.0); }
 MHPC_HD real tangent(Dual a) { return a.d; }
 
+// The short sin / cos reduction's and kernels' constants (below).  A caller may pass a copy
+// held in VGPRs (a knot loop: no per-knot s_mov pairs materialising them, gfx950 has no
+// 64-bit literal operand); the values, hence the results, are the same.
+struct SinCosK {
+  double c[15];
+};
+constexpr SinCosK kSinCosK = {{0.63661977236758138,  // 2 / pi
+                               1.5707963267948966,   // pi/2, high part
+                               6.123233995736766e-17,  // pi/2 - high part
+                               8.33333333332248946124e-03, -1.98412698298579493134e-04,
+                               2.75573137070700676789e-06, -2.50507602534068634195e-08,
+                               1.58969099521155010221e-10, -1.66666666666666324348e-01,
+                               4.16666666666666019037e-02, -1.38888888888741095749e-03,
+                               2.48015872894767294178e-05, -2.75573143513906633035e-07,
+                               2.08757232129817482790e-09, -1.13596475577881948265e-11}};
+
 #ifndef MHPC_FP32
 // sin and cos of a link angle: one Cody-Waite reduction by pi/2 (two-part pi/2, FMA) and
 // the fdlibm kernels on |r| <= pi/4 (< 0.75 ulp each); <= 1.5 ulp overall, checked against
 // long double on |a| <= 60.  About half the instructions of the library sincos, whose
 // reduction carries a double-double and a Payne-Hanek path for huge arguments -- kept here
 // only for |a| > 1e5 (a diverged rollout), where the short reduction loses accuracy.
-MHPC_HD void sin_cos_short(double a, double* s, double* c) {
-  const double k = rint(a * 0.63661977236758138);              // 2 / pi
-  double r = fma(-k, 1.5707963267948966, a);                   // pi/2, high part
-  r = fma(-k, 6.123233995736766e-17, r);                       // pi/2 - high part
+MHPC_HD void sin_cos_short(double a, double* s, double* c, const SinCosK& K = kSinCosK) {
+  const double k = rint(a * K.c[0]);
+  double r = fma(-k, K.c[1], a);
+  r = fma(-k, K.c[2], r);
   const double z = r * r;
-  const double ps = 8.33333333332248946124e-03 +
-                    z * (-1.98412698298579493134e-04 +
-                         z * (2.75573137070700676789e-06 +
-                              z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
-  const double sn = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
-  const double pc =
-      z * (4.16666666666666019037e-02 +
-           z * (-1.38888888888741095749e-03 +
-                z * (2.48015872894767294178e-05 +
-                     z * (-2.75573143513906633035e-07 +
-                          z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double ps = K.c[3] + z * (K.c[4] + z * (K.c[5] + z * (K.c[6] + z * K.c[7])));
+  const double sn = r + (z * r) * (K.c[8] + z * ps);
+  const double pc = z * (K.c[9] + z * (K.c[10] + z * (K.c[11] + z * (K.c[12] + z * (K.c[13] + z * K.c[14])))));
   const double hz = 0.5 * z, w = 1.0 - hz;
   const double cs = w + (((1.0 - w) - hz) + z * pc);
   const int n = (int)k & 3;
@@ -186,12 +194,12 @@ MHPC_HD void sin_cos(real a, real* s, real* c) {
 // (one set of constants, interleaved chains) and one wave-uniform library fallback for them
 // all; per angle the same value as sin_cos.
 template <int N>
-MHPC_HD void sin_cos_n(const real (&a)[N], real (&s)[N], real (&c)[N]) {
+MHPC_HD void sin_cos_n(const real (&a)[N], real (&s)[N], real (&c)[N], const SinCosK& K = kSinCosK) {
 #if !defined(MHPC_FP32) && defined(__HIP_DEVICE_COMPILE__)
   bool big = false;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    sin_cos_short(a[i], &s[i], &c[i]);
+    sin_cos_short(a[i], &s[i], &c[i], K);
     big = big || !(fabs(a[i]) <= 1e5);
   }
   if (__builtin_amdgcn_ballot_w64(big)) {
@@ -205,6 +213,7 @@ MHPC_HD void sin_cos_n(const real (&a)[N], real (&s)[N], real (&c)[N]) {
     }
   }
 #else
+  (void)K;
 #pragma unroll
   for (int i = 0; i < N; ++i) sin_cos(a[i], &s[i], &c[i]);
 #endif

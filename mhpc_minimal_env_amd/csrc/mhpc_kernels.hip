@@ -89,6 +89,10 @@ constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
 #ifndef MHPC_RO_PREFETCH
 #define MHPC_RO_PREFETCH 1
 #endif
+// The pair variant's dynamics wave keeps the sin / cos constants in VGPRs (SinCosK)
+#ifndef MHPC_RO_VCONST
+#define MHPC_RO_VCONST 1
+#endif
 
 // native 2-wide vector (HIP's double2 class defeats register promotion of arrays of it)
 typedef real sreal2 __attribute__((ext_vector_type(2)));
@@ -309,6 +313,15 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // the hand-over instead of heading the next knot's dependent chain; the next chunk is
   // dropped into the stage right after the last knot of a chunk has read it.
   real pK[28], pX[14], pU[4], pD[4];
+  // sin / cos constants: VGPR copies (opaque to the compiler, so it keeps them live instead of
+  // rematerialising each with two s_mov per use in the knot loop)
+  SinCosK scK = kSinCosK;
+#if MHPC_RO_VCONST && !defined(MHPC_FP32)
+  if (PAIR) {
+#pragma unroll
+    for (int i = 0; i < 15; ++i) asm volatile("" : "+v"(scK.c[i]));
+  }
+#endif
   auto prefetch = [&](bool wb, int kk) __attribute__((always_inline)) {
     const int kcc = kk & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
     const int KP = wb ? Stage<true>::KP : Stage<false>::KP, TP = wb ? Stage<true>::TP : Stage<false>::TP;
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
       // the state-only part of the dynamics first: the feedback operands (prefetched from the
       // LDS stage at the end of the previous knot) land meanwhile
       WbPairPrep P;
-      wb_pair_prep(x, back, P);
+      wb_pair_prep(x, back, P, scK);
       // the own leg's two torques (rows 2 back, 2 back + 1 of K)
       real u2[2];
       if (PF) {
@@ -1329,13 +1342,18 @@ __global__ __launch_bounds__(64) void k_init(SolveParams sp, DevBufs d, int warm
   for (int i = 0; i < 14; ++i) x[i] = x0[i];
   const real qnom[4] = {PI / 4, -PI * 7 / 12, PI / 4, -PI * 7 / 12};
   const real Kp[4] = {5 * real(8.0), 5 * real(1.0), 5 * real(12.0), 5 * real(10.0)};
+  SinCosK scK = kSinCosK;  // VGPR copies (see k_rollout)
+#if MHPC_RO_VCONST && !defined(MHPC_FP32)
+#pragma unroll
+  for (int i = 0; i < 15; ++i) asm volatile("" : "+v"(scK.c[i]));
+#endif
   for (int p = 0; p < L.n_wb; ++p) {
     const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
     const real dt = L.dt[p];
     for (int k = 0; k < N - 1; ++k) {
       // the state-only part of the dynamics first: the stance controller reuses its geometry
       WbPairPrep P;
-      wb_pair_prep(x, back, P);
+      wb_pair_prep(x, back, P, scK);
       real u[4];
 #ifdef MHPC_FP32
       // (fp32: the reference-ordered evaluation below; its C5 accuracy is chaotic in the warm

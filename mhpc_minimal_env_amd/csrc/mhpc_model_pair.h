@@ -216,7 +216,7 @@ struct WbPairPrep {
   real hb[3];      // base bias
   PairFactor F;
 };
-MHPC_HD void wb_pair_prep(const real* x, bool back, WbPairPrep& P) {
+MHPC_HD void wb_pair_prep(const real* x, bool back, WbPairPrep& P, const SinCosK& K = kSinCosK) {
   MHPC_NO_FMA_WB
   const real sg = back ? -real(1.0) : real(1.0);
   // geometry: the body pitch and the own leg's two links
@@ -226,7 +226,7 @@ MHPC_HD void wb_pair_prep(const real* x, bool back, WbPairPrep& P) {
   const real a1 = x[2] + qh;
   const real a2 = a1 + qk;
   real sv[3], cv[3];
-  sin_cos_n<3>({x[2], a1, a2}, sv, cv);
+  sin_cos_n<3>({x[2], a1, a2}, sv, cv, K);
   const real sth = sv[0], cth = cv[0];
   L.s1 = sv[1]; L.c1 = cv[1];
   L.s2 = sv[2]; L.c2 = cv[2];
