@@ -80,10 +80,12 @@ int ro_store_default() { return RO_STORE_FIRST; }
 #endif
 constexpr int RO_PAIR_PPB = MHPC_RO_PAIR_PPB;
 
-// Ring depth of the pair variant's dynamics -> cost hand-over (2: a barrier per knot record;
-// 4: one per two records)
+// Ring depth of the pair variant's dynamics -> cost hand-over: a barrier per RD / 2 records
+// (2: per record; 4: per two; 8: per four -- the cost wave takes every record handed over
+// since the last barrier, in knot order.  8 vs 4: line search 0.399 -> 0.394 ms per launch at
+// batch 1024, equal at batch 1, interleaved A/B round 5)
 #ifndef MHPC_RO_RING_PAIR
-#define MHPC_RO_RING_PAIR 4
+#define MHPC_RO_RING_PAIR 8
 #endif
 constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
 #ifndef MHPC_RO_PREFETCH
@@ -232,7 +234,11 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   constexpr int RD = PIPE ? (PAIR ? RO_RING_PAIR : 2) : 1;
   constexpr int RG = PIPE ? RD / 2 : 1;  // records per barrier
   static_assert(RG >= 1 && (RG & (RG - 1)) == 0, "ring depth");
-  __shared__ real ring[RD][RING_W][64];
+  // (the pair variant's records belong to its <= 32 candidates: half the columns suffice; a
+  // deeper ring takes them, the four-deep one keeps 64 -- with its LDS cut to 52 KB a third
+  // block fits a CU and the line search measured 0.5 % slower)
+  constexpr int RCOL = (PAIR && RD > 4) ? 32 : 64;
+  __shared__ real ring[RD][RING_W][RCOL];
   __shared__ acc sJ[64], sViol[64], sV[MAXP][64];
   __shared__ real sH[MAXP][64];
   __shared__ int sAny;
@@ -678,7 +684,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         constexpr int nrec = wb ? RING_W : 14;
         const CostPhase c = cost_phase_begin(WBc, p);
         acc V = 0;
-        int pend = -1;  // a knot record handed over but not consumed yet (RG > 1)
+        int npend = 0;  // knot records handed over since the last barrier, not consumed yet
         for (int k = 0; k < N - 1; ++k, ++q) {
           const int s = q & (RD - 1);
           const bool bar = (q & (RG - 1)) == RG - 1;
@@ -692,9 +698,9 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
 #endif
             if (run) {
               real r[RING_W];
-              if (RG > 1 && pend >= 0) {
-                ring_rec((s - 1) & (RD - 1), r, nrec);
-                cost_knot(WBc, p, c, pend, r, V);
+              for (int i = npend; i >= 1; --i) {  // (knot order: the serial rollout's sum)
+                ring_rec((s - i) & (RD - 1), r, nrec);
+                cost_knot(WBc, p, c, k - i, r, V);
               }
               ring_rec(s, r, nrec);
               cost_knot(WBc, p, c, k, r, V);
@@ -707,16 +713,16 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
             }
 #endif
           }
-          if (RG > 1) pend = bar ? -1 : k;  // RG = 2: at most one record waits
+          npend = bar ? 0 : npend + 1;  // (< RG)
         }
         const int s = q & (RD - 1);
         ++q;
         __syncthreads();
         if (run) {
           real r[RING_W];
-          if (RG > 1 && pend >= 0) {  // the phase's last knot record, if still waiting
-            ring_rec((s - 1) & (RD - 1), r, nrec);
-            cost_knot(WBc, p, c, N - 2, r, V);
+          for (int i = npend; i >= 1; --i) {  // the phase's last knot records still waiting
+            ring_rec((s - i) & (RD - 1), r, nrec);
+            cost_knot(WBc, p, c, N - 1 - i, r, V);
           }
           ring_rec(s, r, wb ? 14 : 6);
           cost_terminal(WBc, p, c, r, V);
