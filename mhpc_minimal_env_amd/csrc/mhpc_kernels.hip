@@ -91,7 +91,7 @@ constexpr int RO_RING_PAIR = MHPC_RO_RING_PAIR;
 #ifndef MHPC_RO_PREFETCH
 #define MHPC_RO_PREFETCH 1
 #endif
-// The pair variant's dynamics wave keeps the sin / cos constants in VGPRs (SinCosK)
+// The line search's dynamics keeps the sin / cos constants in registers (SinCosK)
 #ifndef MHPC_RO_VCONST
 #define MHPC_RO_VCONST 1
 #endif
@@ -323,10 +323,8 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
   // rematerialising each with two s_mov per use in the knot loop)
   SinCosK scK = kSinCosK;
 #if MHPC_RO_VCONST && !defined(MHPC_FP32)
-  if (PAIR) {
 #pragma unroll
-    for (int i = 0; i < 15; ++i) asm volatile("" : "+v"(scK.c[i]));
-  }
+  for (int i = 0; i < 15; ++i) asm volatile("" : "+v"(scK.c[i]));
 #endif
   auto prefetch = [&](bool wb, int kk) __attribute__((always_inline)) {
     const int kcc = kk & ((wb ? Stage<true>::CH : Stage<false>::CH) - 1);
@@ -451,7 +449,7 @@ __global__ __launch_bounds__(PIPE ? 128 : 64) void k_rollout(SolveParams sp, Dev
         u[i] = (nk[14 + i] + eps * duk[i]) + fb;
       }
       real xd[14], y[4];
-      wb_dynamics<real>(x, u, mode, xd, y);
+      wb_dynamics<real>(x, u, mode, xd, y, scK);
 #pragma unroll
       for (int i = 0; i < 14; ++i) rr[i] = x[i];
 #pragma unroll

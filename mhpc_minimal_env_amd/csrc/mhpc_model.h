@@ -96,17 +96,18 @@ struct WbGeo {
 // BATCH: the real-valued angles through sin_cos_n (fewer instructions; more live registers,
 // so the register-bound partials keep the one-at-a-time form).  Same values either way.
 template <class Q, class V, bool BATCH = true>
-MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g) {
+MHPC_HD void wb_geometry(const Q* xq, const V* xv, WbGeo<Q, V>& g, const SinCosK& K = kSinCosK) {
   if constexpr (BATCH && std::is_same<Q, real>::value) {
     // the five link angles' sines / cosines side by side (sin_cos_n)
     const real a[5] = {xq[2], xq[2] + xq[3], (xq[2] + xq[3]) + xq[4], xq[2] + xq[5],
                        (xq[2] + xq[5]) + xq[6]};
     real sv[5], cv[5];
-    sin_cos_n<5>(a, sv, cv);
+    sin_cos_n<5>(a, sv, cv, K);
     g.sth = sv[0]; g.cth = cv[0];
     g.leg[0].s1 = sv[1]; g.leg[0].c1 = cv[1]; g.leg[0].s2 = sv[2]; g.leg[0].c2 = cv[2];
     g.leg[1].s1 = sv[3]; g.leg[1].c1 = cv[3]; g.leg[1].s2 = sv[4]; g.leg[1].c2 = cv[4];
   } else {
+    (void)K;
     sin_cos(xq[2], &g.sth, &g.cth);
     for (int f = 0; f < 2; ++f) {
       const int ih = 3 + 2 * f, ik = 4 + 2 * f;
@@ -383,9 +384,10 @@ MHPC_HD void wb_stance(const V* xv, const WbGeo<Q, V>& g, const Q M[28],
 // zero in flight.  mode 1: back stance (Dyn_BS), 2/4: flight (Dyn_FL), 3: front stance
 // (Dyn_FS).
 template <class Q, class V>
-MHPC_HD void wb_dynamics_qv(const Q* xq, const V* xv, const V* u, int mode, V* xdot, V* y) {
+MHPC_HD void wb_dynamics_qv(const Q* xq, const V* xv, const V* u, int mode, V* xdot, V* y,
+                            const SinCosK& K = kSinCosK) {
   WbGeo<Q, V> g;
-  wb_geometry<Q, V>(xq, xv, g);
+  wb_geometry<Q, V>(xq, xv, g, K);
   Q M[28];
   V h[7];
   wb_mass_bias<Q, V>(xv, g, M, h);
@@ -409,8 +411,8 @@ MHPC_HD void wb_dynamics_qv(const Q* xq, const V* xv, const V* u, int mode, V* x
 
 // The plain interface: x = (q, qdot) in one scalar type.
 template <class S>
-MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y) {
-  wb_dynamics_qv<S, S>(x, x + 7, u, mode, xdot, y);
+MHPC_HD void wb_dynamics(const S* x, const S* u, int mode, S* xdot, S* y, const SinCosK& K = kSinCosK) {
+  wb_dynamics_qv<S, S>(x, x + 7, u, mode, xdot, y, K);
 }
 
 // ---- Jacobians by implicit differentiation (the partials kernel, Dyn_*_par) --------------
