@@ -1715,6 +1715,57 @@ hipError_t launch_cost(const SolveParams& sp, const DevBufs& d, int al_iter, hip
   return hipGetLastError();
 }
 
+// The line search's launch shape for a batch (the variant launch_rollout takes)
+struct RoShape {
+  bool pair, pipe, st;
+  int nblk, nblk2;
+};
+static RoShape ro_shape(const SolveParams& sp) {
+  RoShape r;
+  const int ppw = 64 / sp.n_cand;
+  r.nblk = (int)grid_of(sp, ppw);
+  const int ncu = sp.ncu;
+#ifdef MHPC_RO_PIPE
+  r.pipe = MHPC_RO_PIPE;
+#else
+  r.pipe = r.nblk <= 2 * ncu;  // measured crossover: beyond it the second
+                               // wave per block only competes for issue slots
+#endif
+  // staged: ST_PPW problems per wave at most, and every phase within the reference stage
+  const bool fits = sp.stage_fits != 0;
+  r.st = ppw <= ST_PPW && fits;
+  // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
+  const int ppw2 = std::min(32 / sp.n_cand, RO_PAIR_PPB);
+  r.nblk2 = ppw2 > 0 ? (int)grid_of(sp, ppw2) : 0;
+#ifdef MHPC_RO_PAIR_MAX_BLK
+  const int pair_max = MHPC_RO_PAIR_MAX_BLK;
+#else
+  const int pair_max = 2 * ncu;
+#endif
+  r.pair = r.pipe && r.st && ppw2 > 0 && r.nblk2 <= pair_max;
+  if (sp.var_ro) {  // forced (mhpc_set_kernel_variant checked that it applies)
+    const int v = sp.var_ro;
+    r.pair = v == MHPC_VARIANT_RO_PAIR;
+    r.pipe = r.pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_PIPE;
+    r.st = r.pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_FUSED_STAGED;
+    if (!fits) r.pair = r.st = false;  // a phase longer than the stage: the unstaged form
+  }
+  return r;
+}
+
+// Trials that store their running records by default, for the shape the batch takes: the
+// two-wave shapes (up to ~2k problems: the line search is a latency chain and a re-roll
+// launch is another one) store the first RO_STORE_FIRST; the one-wave shape (the chip full,
+// record stores a large part of the launch) the first two when the batch has one layout --
+// interleaved A/B round 5: C3 at 4096 344.4k / 345.1k -> 348.3k / 350.5k solves/s (3 stored:
+// +0.6 %), C5 at 4096 110.6k -> 118.4k, C3 at 1024 188.0k -> 172.6k with 2.  A mixed batch
+// keeps RO_STORE_FIRST (134.2k -> 127.5k with 2): its re-roll launch, needed when any problem
+// accepts an unstored trial, lasts as long as its longest layout's chain.
+int ro_store_auto(const SolveParams& sp) {
+  const RoShape r = ro_shape(sp);
+  return (r.pipe || sp.ngrp > 1) ? RO_STORE_FIRST : 2;
+}
+
 hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, int ddp_iter,
                           int max_ddp, int full, hipStream_t s) {
   if (full) {
@@ -1722,34 +1773,9 @@ hipError_t launch_rollout(const SolveParams& sp, const DevBufs& d, int al_iter, 
                        sp, d, al_iter, 0, 0, 1);
     return hipGetLastError();
   }
-  const int ppw = 64 / sp.n_cand;
-  const int nblk = (int)grid_of(sp, ppw);
-  const int ncu = sp.ncu;
-#ifdef MHPC_RO_PIPE
-  bool pipe = MHPC_RO_PIPE;
-#else
-  bool pipe = nblk <= 2 * ncu;  // measured crossover: beyond it the second
-                                // wave per block only competes for issue slots
-#endif
-  // staged: ST_PPW problems per wave at most, and every phase within the reference stage
-  const bool fits = sp.stage_fits != 0;
-  bool st = ppw <= ST_PPW && fits;
-  // lane pairs (two lanes per candidate) while the chip has SIMDs to spare for them
-  const int ppw2 = std::min(32 / sp.n_cand, RO_PAIR_PPB);
-  const int nblk2 = ppw2 > 0 ? (int)grid_of(sp, ppw2) : 0;
-#ifdef MHPC_RO_PAIR_MAX_BLK
-  const int pair_max = MHPC_RO_PAIR_MAX_BLK;
-#else
-  const int pair_max = 2 * ncu;
-#endif
-  bool pair = pipe && st && ppw2 > 0 && nblk2 <= pair_max;
-  if (sp.var_ro) {  // forced (mhpc_set_kernel_variant checked that it applies)
-    const int v = sp.var_ro;
-    pair = v == MHPC_VARIANT_RO_PAIR;
-    pipe = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_PIPE;
-    st = pair || v == MHPC_VARIANT_RO_PIPE_STAGED || v == MHPC_VARIANT_RO_FUSED_STAGED;
-    if (!fits) pair = st = false;  // a phase longer than the stage: the unstaged form
-  }
+  const RoShape r = ro_shape(sp);
+  const bool pair = r.pair, pipe = r.pipe, st = r.st, fits = sp.stage_fits != 0;
+  const int nblk = r.nblk, nblk2 = r.nblk2;
   if (pair)
     hipLaunchKernelGGL((k_rollout<true, true, true>), dim3(nblk2), dim3(128), 0, s, sp, d, al_iter,
                        ddp_iter, max_ddp, 0);

@@ -25,6 +25,7 @@ hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t, hipS
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
 bool bws_split(const SolveParams&);
 int ro_store_default();
+int ro_store_auto(const SolveParams&);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
 hipError_t launch_reset(const SolveParams&, const DevBufs&, hipStream_t);
 hipError_t launch_store(const SolveParams&, const DevBufs&, real*, int, int, int, hipStream_t);
@@ -137,6 +138,7 @@ struct Handle {
   // sub-batches (MHPC_VARIANT_SUBBATCH): the solve schedule runs once per contiguous block of
   // problems, each block on its own stream pair; created on first use
   int nsub_req = 0;
+  int ro_store_req = 0;  // MHPC_VARIANT_RO_STORE (0: by the batch's line-search shape)
   struct SubStreams {
     hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // s3: the partials' second group
     hipEvent_t fork = nullptr, join = nullptr, gate = nullptr, done = nullptr, pfork = nullptr,
@@ -823,6 +825,8 @@ static int ensure_sub_streams(Handle* h, int n) {
 }
 
 static int solve_async(Handle* h) {
+  // stored line-search trials for this batch's launch shape (unless set by the caller)
+  if (!h->ro_store_req) h->sp.ro_store = ro_store_auto(h->sp);
   const std::vector<SolveOp> ops = solve_ops(h);
   const int nops = (int)ops.size();
   const int nsub = sub_batches(h);
@@ -1367,7 +1371,8 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
   }
   if (which == MHPC_VARIANT_RO_STORE) {
     if (variant < 0 || variant > MAXC) return fail(MHPC_ERR_INVALID, "stored trials must be 0..32");
-    sp.ro_store = variant ? variant : ro_store_default();
+    h->ro_store_req = variant;
+    sp.ro_store = variant ? variant : ro_store_auto(sp);
     return MHPC_OK;
   }
   if (which == MHPC_VARIANT_SUBBATCH) {
