@@ -138,7 +138,9 @@ int mhpc_get_phase(mhpc_handle* h, int phase, double* x, double* u, double* y, d
  * _phases[p]->get_nominal_ms_ptr() / get_CTG_info_ptr() hold it (SinglePhaseAbstract.h:79-81). */
 int mhpc_get_phase_problems(mhpc_handle* h, int phase, int first, int count, double* x, double* u,
                             double* y, double* K, double* du, double* Vx);
-/* J, dV_exp, viol: [batch]; V_phase, dV_phase: [batch][n_phases]; trace: [batch][MHPC_TRACE_LEN]
+/* J, dV_exp, viol: [batch]; V_phase, dV_phase: [batch][P] with P = mhpc_max_phases (the
+ * largest phase count over the problems' layouts -- not mhpc_get_desc's n_wb + n_fb, which is
+ * problem 0's; entries past a problem's own phases are zero); trace: [batch][MHPC_TRACE_LEN]
  * (decision trace, encoding in DESIGN.md §Parity); any pointer may be NULL. */
 int mhpc_get_scalars(mhpc_handle* h, double* J, double* dV_exp, double* viol, double* V_phase,
                      double* dV_phase, int32_t* trace);
@@ -195,6 +197,9 @@ int mhpc_update_problems(mhpc_handle* h, int n_gaits, const mhpc_gait* gaits,
                          const int32_t* gait_of_problem, const int32_t* steps);
 /* Distinct phase layouts currently in use (1 for a homogeneous batch). */
 int mhpc_num_layouts(mhpc_handle* h, int* n);
+/* The largest phase count over the problems' current layouts: the row length of
+ * mhpc_get_scalars' V_phase / dV_phase. */
+int mhpc_max_phases(mhpc_handle* h, int* n);
 
 /* ---- cost and constraint parameters (the reference's downward plugin points) --------
  * The reference's solve reads its weights through CostAbstract / Cost<T,X,U,Y>

@@ -466,11 +466,9 @@ class MHPCLocomotion {
       mixed = mixed || std::memcmp(&ds[b], &ds[0], sizeof(mhpc_problem_desc)) != 0;
     }
     xw_ = 6;
-    pmax_ = 0;
-    for (const mhpc_problem_desc& d : ds) {
+    for (const mhpc_problem_desc& d : ds)
       if (d.n_wb > 0) xw_ = 14;
-      pmax_ = std::max(pmax_, d.n_wb + d.n_fb);
-    }
+    check(mhpc_max_phases(h_, &pmax_), "mhpc_max_phases");
     desc_ = ds[problem_];
     pdesc_ = mixed ? std::move(ds) : std::vector<mhpc_problem_desc>();
     refresh_phases(false);

@@ -200,6 +200,7 @@ SIGNATURES = [
     ("mhpc_get_problem_desc", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                              ctypes.POINTER(ProblemDesc)]),
     ("mhpc_num_layouts", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    ("mhpc_max_phases", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     ("mhpc_rollout_costs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _DP, _DP, _DP,
                                           ctypes.POINTER(ctypes.c_float)]),
     ("mhpc_destroy", None, [ctypes.c_void_p]),

@@ -22,6 +22,7 @@ int api_update_problems(Handle* h, int n_gaits, const mhpc_gait* gaits, const in
 int api_set_layouts(Handle* h, int n_desc, const mhpc_problem_desc* descs, const int32_t* lop);
 int api_get_problem_desc(Handle* h, int b, mhpc_problem_desc* desc);
 int api_num_layouts(Handle* h, int* n);
+int api_max_phases(Handle* h, int* n);
 int api_get_desc(Handle* h, mhpc_problem_desc* desc);
 int api_get_counters(Handle* h, mhpc_counters* c);
 int api_set_profiling(Handle* h, int on);

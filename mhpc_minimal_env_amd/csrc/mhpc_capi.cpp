@@ -150,6 +150,7 @@ extern "C" int mhpc_get_problem_desc(mhpc_handle* h, int problem, mhpc_problem_d
   FWD(get_problem_desc, problem, desc);
 }
 extern "C" int mhpc_num_layouts(mhpc_handle* h, int* n) { FWD(num_layouts, n); }
+extern "C" int mhpc_max_phases(mhpc_handle* h, int* n) { FWD(max_phases, n); }
 extern "C" int mhpc_get_counters(mhpc_handle* h, mhpc_counters* c) { FWD(get_counters, c); }
 extern "C" int mhpc_set_profiling(mhpc_handle* h, int on) { FWD(set_profiling, on); }
 extern "C" int mhpc_get_kernel_stats(mhpc_handle* h, double* ms, int64_t* launches,

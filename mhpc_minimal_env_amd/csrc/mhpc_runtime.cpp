@@ -280,24 +280,44 @@ static mhpc_problem_desc norm_desc(const mhpc_problem_desc& in) {
 }
 
 // The packed per-knot arrays for a knot stride of NK (grown, never shrunk: their content is
-// rebuilt by initialize / update_problem; the partials records' zero columns are zeroed here
-// once, no kernel writes them).
+// rebuilt by initialize / update_problem).  The partials records' zero columns (x, z, xdot,
+// zdot) are written by no kernel: they are zeroed here whenever the stride changes, since the
+// column blocks are stride-major (par_col) and a new stride moves them onto words the old
+// stride used for other columns.  New arrays are allocated before the old ones are freed, so
+// a failed allocation leaves the handle's arrays and stride as they were.
 static int ensure_knot_arrays(Handle* h, int NK) {
-  if (NK <= h->nk_cap) return MHPC_OK;
   DevBufs& d = h->d;
   const size_t B = h->sp.B, nk = NK;
+  const bool grow = NK > h->nk_cap;
+  if (!grow && NK == h->sp.NK) return MHPC_OK;
   HIPCHK(hipStreamSynchronize(h->stream));
-  real** arr[] = {&d.traj, &d.refpos, &d.K, &d.du, &d.G, &d.par, &d.out};
-  const size_t per[] = {(size_t)h->sp.nslot * KS, 1, 56, 4, 14, PS, KS};
-  for (int i = 0; i < 7; ++i) {
-    if (*arr[i]) HIPCHK(hipFree(*arr[i]));
-    *arr[i] = nullptr;
-    HIPCHK(hipMalloc((void**)arr[i], B * nk * per[i] * sizeof(real)));
+  HIPCHK(hipStreamSynchronize(h->stream2));
+  HIPCHK(hipStreamSynchronize(h->stream3));
+  for (const Handle::SubStreams& s : h->subs) {
+    if (s.s1) HIPCHK(hipStreamSynchronize(s.s1));
+    if (s.s2) HIPCHK(hipStreamSynchronize(s.s2));
+    if (s.s3) HIPCHK(hipStreamSynchronize(s.s3));
   }
-  HIPCHK(hipMemsetAsync(d.traj, 0, B * h->sp.nslot * nk * KS * sizeof(real), h->stream));
+  if (grow) {
+    real** arr[] = {&d.traj, &d.refpos, &d.K, &d.du, &d.G, &d.par, &d.out};
+    const size_t per[] = {(size_t)h->sp.nslot * KS, 1, 56, 4, 14, PS, KS};
+    real* fresh[7] = {};
+    for (int i = 0; i < 7; ++i) {
+      const hipError_t e = hipMalloc((void**)&fresh[i], B * nk * per[i] * sizeof(real));
+      if (e != hipSuccess) {
+        for (int j = 0; j < i; ++j) (void)hipFree(fresh[j]);
+        return fail(MHPC_ERR_DEVICE, std::string("knot array allocation failed: ") + hipGetErrorString(e));
+      }
+    }
+    for (int i = 0; i < 7; ++i) {
+      if (*arr[i]) (void)hipFree(*arr[i]);
+      *arr[i] = fresh[i];
+    }
+    h->nk_cap = NK;
+    HIPCHK(hipMemsetAsync(d.traj, 0, B * h->sp.nslot * nk * KS * sizeof(real), h->stream));
+  }
   HIPCHK(hipMemsetAsync(d.par, 0, B * nk * PS * sizeof(real), h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  h->nk_cap = NK;
   return MHPC_OK;
 }
 
@@ -1240,8 +1260,10 @@ int api_update_problems(Handle* h, int n_gaits, const mhpc_gait* gaits, const in
         NK += nd.N[p];
       }
       if (NK > MHPC_MAX_KNOTS) return fail(MHPC_ERR_INVALID, "too many knots");
-      npl[b].rot_wb += 1;  // pidx_WB / pidx_FB: front -> back (MHPCLocomotion.cpp:111-121)
-      npl[b].rot_fb += 1;
+      // pidx_WB / pidx_FB: front -> back (MHPCLocomotion.cpp:111-121); kept reduced, so a
+      // long receding-horizon loop never overflows the count
+      npl[b].rot_wb = (npl[b].rot_wb + 1) % std::max(nd.n_wb, 1);
+      npl[b].rot_fb = (npl[b].rot_fb + 1) % std::max(nd.n_fb, 1);
     }
   }
   // phases write through to their buffers in the reference: save the current layouts
@@ -1315,6 +1337,13 @@ int api_get_problem_desc(Handle* h, int b, mhpc_problem_desc* desc) {
 int api_num_layouts(Handle* h, int* n) {
   if (!h || !n) return fail(MHPC_ERR_INVALID, "null argument");
   *n = h->sp.ngrp;
+  return MHPC_OK;
+}
+
+// the row length of get_scalars' V_phase / dV_phase (rebuild_groups: sp.pmax)
+int api_max_phases(Handle* h, int* n) {
+  if (!h || !n) return fail(MHPC_ERR_INVALID, "null argument");
+  *n = h->sp.pmax;
   return MHPC_OK;
 }
 

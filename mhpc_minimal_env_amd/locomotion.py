@@ -354,6 +354,13 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_num_layouts(self._h, ctypes.byref(n)), "mhpc_num_layouts")
         return n.value
 
+    def max_phases(self) -> int:
+        """Row length of get_scalars' per-phase arrays (mhpc_max_phases)."""
+        import ctypes
+        n = ctypes.c_int(0)
+        capi.check(capi.lib().mhpc_max_phases(self._h, ctypes.byref(n)), "mhpc_max_phases")
+        return n.value
+
     def _refresh_descs(self):
         ds = [self.problem_desc(b) for b in range(self.batch)]
         key = lambda d: bytes(d)
@@ -462,7 +469,7 @@ class MHPCLocomotion:
 
     def get_scalars(self) -> dict:
         B = self.batch
-        P = max(d.n_phases for d in (self.descs or [self.desc]))  # rows of the most phases
+        P = self.max_phases()  # rows of the most phases over the problems' layouts
         out = {"J": np.zeros(B), "dV_exp": np.zeros(B), "viol": np.zeros(B),
                "V": np.zeros((B, P)), "dV": np.zeros((B, P)),
                "trace": np.zeros((B, capi.MHPC_TRACE_LEN), dtype=np.int32)}

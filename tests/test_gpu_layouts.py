@@ -312,3 +312,40 @@ def test_fleet_cpp_example(need_gpu, tmp_path):
         assert int(nph) == d.n_wb + d.n_fb
         got = [tuple(int(v) for v in m.split("/")) for m in modes.split()]
         assert got == [(d.mode_seq[p], d.N[p]) for p in range(d.n_wb + d.n_fb)]
+
+
+def test_shrinking_knot_stride_bitwise_vs_fresh_handle(need_gpu):
+    """The partials records are column-block major with the handle's knot stride (the largest
+    knot count over its layouts), and their zero columns are written by no kernel.  A handle
+    that solved a long layout (C5, 534 + WB knots) and is then given a shorter one (C3) must
+    solve bitwise like a fresh C3 handle -- the zero columns re-zeroed for the new stride
+    (ADVICE r5).  Also: mhpc_max_phases is the row length of the per-phase scalars."""
+    from mhpc_minimal_env_amd import configs, locomotion as L
+    c3, c5 = configs.c3_desc(), configs.c5_desc()
+    B = 24
+    x0 = configs.x0_rows([c3], np.zeros(B, dtype=np.int32))
+    fresh = solve_homog(c3, x0)
+    loco = L.MHPCLocomotion(desc=c5, option=L.HSDDP_OPTION(), batch=B, device=0)
+    try:
+        lop = (np.arange(B) % 2).astype(np.int32)
+        loco.set_layouts([c5, c3], lop)
+        assert loco.max_phases() == c5.n_phases
+        loco.set_initial_condition(configs.x0_rows([c5, c3], lop))
+        loco.initialization()
+        loco.solve_mhpc()
+        loco.set_layouts([c3], np.zeros(B, dtype=np.int32))
+        assert loco.max_phases() == c3.n_phases
+        loco.set_initial_condition(x0)
+        loco.initialization()
+        status = loco.solve_mhpc().copy()
+        sc = loco.get_scalars()
+        assert sc["V"].shape == (B, c3.n_phases)
+        for b in range(B):
+            got = loco.problem_concatenated(b)
+            for k in ARR:
+                np.testing.assert_array_equal(got[k], fresh[k][b], err_msg=f"problem {b}: {k}")
+        for k in ("J", "dV_exp", "viol", "V", "dV", "trace"):
+            np.testing.assert_array_equal(sc[k], fresh[k], err_msg=k)
+        np.testing.assert_array_equal(status, fresh["status"])
+    finally:
+        loco.close()
