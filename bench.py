@@ -600,6 +600,31 @@ def main():
                   "ms_per_step": d4 / args.steps * 1e3, "steps": args.steps,
                   "note": "same step (initialization + solve of the whole batch) at the north-star "
                           "batch, timed after the headline's timed region"}
+        # mixed: the alternative to one handle of per-problem layouts -- one homogeneous handle
+        # per layout holding that layout's problems (same x0 rows), stepped one after the other
+        # (each step = init + solve of every handle), timed in this run after the headline
+        serial = None
+        if world == 1 and args.workload == "mixed" and dist is None:
+            descs, lop = layouts_of("mixed", B)
+            hs = [Solver(descs[l], opt, x0[lop == l], local_rank) for l in range(len(descs))
+                  if (lop == l).any()]
+            for _ in range(args.warmup):
+                for h in hs:
+                    h.step()
+            torch.cuda.synchronize()
+            t5 = time.perf_counter()
+            for _ in range(args.steps):
+                for h in hs:
+                    h.step()
+            torch.cuda.synchronize()
+            d5 = time.perf_counter() - t5
+            for h in hs:
+                h.close()
+            serial = {"handles": len(hs), "value": B * args.steps / d5, "unit": "solves/s",
+                      "ms_per_step": d5 / args.steps * 1e3,
+                      "mixed_over_serial": (total / dt) / (B * args.steps / d5),
+                      "note": "same problems, one homogeneous handle per layout, stepped in turn "
+                              "(init + solve each), timed after the headline's timed region"}
         cpu, why = (None, "disabled" if world == 1 else "reported at N=1 only")
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or usable_cpus()
@@ -637,6 +662,8 @@ def main():
         }
         if ns is not None:
             line["north_star_b4096"] = ns
+        if serial is not None:
+            line["serial_homogeneous"] = serial
         if shard is not None:
             line["sharding"] = shard
         print(json.dumps(line), file=_LINE_OUT or sys.stdout, flush=True)

@@ -56,10 +56,26 @@ namespace MHPC_NS {
 #ifndef MHPC_BWS_WIDE
 #define MHPC_BWS_WIDE 1
 #endif
+// Arithmetic type of the whole sweep (MHPC_BWS_F64, default): double in both builds.  The fp32
+// build reads its float records and writes float gains, but sums, factors and carries the
+// value function in double -- on MI355X an fp64 FMA issues at the fp32 rate (no packed math in
+// this code), so the fp32 sweep was never faster than the fp64 one, and its rounding was the
+// largest source of the fp32 solve's error (tools/diag_fp32_stages.py; round 6: the round-5
+// codegen change that moved one ill-conditioned C5 problem's G error from 2.5e-2 to 6.2e-2 was
+// rounding of the fp32 sweep, tools/fp32_bisect.py).  Built with -DMHPC_BWS_F64=0 the fp32
+// sweep computes in float with the control block in double (MHPC_BWS_WIDE), as in round 5.
+#ifndef MHPC_BWS_F64
+#define MHPC_BWS_F64 1
+#endif
+#if defined(MHPC_FP32) && MHPC_BWS_F64
+using breal = double;
+#else
+using breal = real;
+#endif
 #if defined(MHPC_FP32) && MHPC_BWS_WIDE
 using wreal = double;
 #else
-using wreal = real;
+using wreal = breal;
 #endif
 
 template <int I>
@@ -154,17 +170,17 @@ __device__ __forceinline__ float recip(float a) {
 // the lower triangle.  By Sylvester's law of inertia its pivots have the signs of Eigen's
 // pivoted factorisation's whenever no pivot is exactly zero, so the verdict is the same; a
 // zero pivot leaves its column, as in Eigen (tests/test_psd_verdict.py).
-__device__ __forceinline__ bool ldlt_nopiv_is_positive4(real* A) {
+__device__ __forceinline__ bool ldlt_nopiv_is_positive4(breal* A) {
   bool neg = false;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const real akk = A[k * 5];
-    neg = neg || akk < real(0.0);
+    const breal akk = A[k * 5];
+    neg = neg || akk < breal(0.0);
     // a zero pivot leaves its column (r = 0: the updates subtract exact zeros)
-    const real r = akk != real(0.0) ? recip(akk) : real(0.0);
+    const breal r = akk != breal(0.0) ? recip(akk) : breal(0.0);
 #pragma unroll
     for (int i = k + 1; i < 4; ++i) {
-      const real l = A[i * 4 + k] * r;
+      const breal l = A[i * 4 + k] * r;
 #pragma unroll
       for (int j = k + 1; j <= i; ++j) A[i * 4 + j] -= l * A[j * 4 + k];
     }
@@ -193,6 +209,32 @@ struct Ldl4 {
     l32 = u32 * r2;
     r3 = recip(((q[3][3] - l30 * q[3][0]) - l31 * u31) - l32 * u32);
   }
+  // The same factorisation with the PSD test folded in (round 6).  ldlt_nopiv_is_positive4 on
+  // Quu - eps I runs exactly these operations on exactly these entries (its elimination order
+  // is this one's), so one instruction stream does both: every lane factors Quu for the solve
+  // except the lane where psd_lane holds, which factors Quu - shift I with the test's zero-pivot
+  // rule and returns its verdict in neg (pivot < 0).  That lane must hold no matrix row the knot
+  // needs (its K, du, H are garbage, but finite).  One factorisation per knot instead of two.
+  __device__ __forceinline__ Ldl4(const T (&q)[4][4], T shift, bool psd_lane, bool& neg) {
+    auto piv = [&](T a) { return (a != T(0.0) || !psd_lane) ? recip(a) : T(0.0); };
+    const T a00 = q[0][0] - shift;
+    r0 = piv(a00);
+    l10 = q[1][0] * r0;
+    l20 = q[2][0] * r0;
+    l30 = q[3][0] * r0;
+    const T a11 = (q[1][1] - shift) - l10 * q[1][0];
+    r1 = piv(a11);
+    const T u21 = q[2][1] - l20 * q[1][0], u31 = q[3][1] - l30 * q[1][0];
+    l21 = u21 * r1;
+    l31 = u31 * r1;
+    const T a22 = ((q[2][2] - shift) - l20 * q[2][0]) - l21 * u21;
+    r2 = piv(a22);
+    const T u32 = (q[3][2] - l30 * q[2][0]) - l31 * u21;
+    l32 = u32 * r2;
+    const T a33 = (((q[3][3] - shift) - l30 * q[3][0]) - l31 * u31) - l32 * u32;
+    r3 = piv(a33);
+    neg = a00 < T(0.0) || a11 < T(0.0) || a22 < T(0.0) || a33 < T(0.0);
+  }
   // x = -Quu^-1 b
   __device__ __forceinline__ void neg_solve(const T (&b)[4], T (&x)[4]) const {
     const T z0 = b[0];
@@ -207,6 +249,35 @@ struct Ldl4 {
   }
 };
 
+// The knot's control block: factor for the solve and the PSD verdict of
+// Eigen::LDLT(Quu - 1e-9 I).isPositive() (SinglePhase.cpp:202-209), row-uniform.  Lane 15 of
+// each 16-lane row runs the PSD test inside the shared factorisation (Ldl4 above): it is an
+// SRB row's filler lane, or the whole-body sweep's second control lane, whose K and H rows are
+// never stored or broadcast.  MHPC_BWS_PSD_SEPARATE=1: the test as its own factorisation (the
+// round-5 form; same verdicts and factors bit for bit, tests/test_gpu_variants.py).
+#ifndef MHPC_BWS_PSD_SEPARATE
+#define MHPC_BWS_PSD_SEPARATE 0
+#endif
+template <class W>
+__device__ __forceinline__ Ldl4<W> control_factor(const W (&q)[4][4], breal eps9, int t, bool& psd) {
+  if constexpr (MHPC_BWS_PSD_SEPARATE || !std::is_same<W, breal>::value) {
+    breal A[16];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) A[a * 4 + c] = breal(q[a][c]) - (a == c ? eps9 : breal(0.0));
+    psd = ldlt_nopiv_is_positive4(A);
+    return Ldl4<W>(q);
+  } else {
+    const bool pl = t == 15;
+    bool neg;
+    const Ldl4<W> F(q, pl ? W(eps9) : W(0.0), pl, neg);
+    // lane 15's verdict to its row (row_newbcast:15)
+    psd = __builtin_amdgcn_update_dpp(0, neg ? 1 : 0, 0x150 + 15, 0xf, 0xf, false) == 0;
+    return F;
+  }
+}
+
 // Ordering point of this wave's LDS accesses for the Qxx transpose: every row's writes (and
 // the diagonal's atomic add) before the reads of the other rows' columns, and those reads
 // before the next knot's writes.  One wave's LDS operations complete in issue order, so the
@@ -220,13 +291,49 @@ __device__ __forceinline__ void wave_lds_order() {
 }
 
 // Per-row LDS: the knot's Q rows for the Qxx transpose, and the value function at phase
-// boundaries (row-major by state index, pitch MP reals: 16-byte aligned rows).
-constexpr int MP = sizeof(real) == 8 ? 18 : 20;
+// boundaries.  Entry (r, c) of the 16 x 16 block lives at M[at(r, c)] = M[c * MP + r]: column-
+// major with an even pitch of 18 reals, and the RowLds of adjacent problems an odd number of
+// reals apart.  Then (tools/lds_banks.py, the banking table of MI355X_MICROARCH.md "LDS"):
+//  * a row write (lane rho stores (rho, j) for one j; 16-lane groups, 32 banks) touches 16
+//    consecutive words: conflict-free;
+//  * a transposed read (lane c loads (j, c) as one ds_read_b64, 32-lane groups over 64 banks):
+//    the 16 columns of one row sit on 16 distinct even word slots (18 c mod 32); the other half
+//    of the group reads row j + 7 (two-row layout: odd slots) or the next problem's block (odd
+//    offset): conflict-free.  fp32 (ds_read_b32, 32 banks): the same;
+//  * the diagonal's atomic add (rho, rho) at 19 rho: 16 distinct slots.
+// (Round 5: row-major, pitch 18 -- rows rho and rho + 8 on the same banks -- 34 % of the WB
+// sweep's LDS cycles were bank conflicts.)  The reads must stay single 8-byte reads: as
+// ds_read2_b64 / b128 pairs (what the compiler merges neighbouring reads into) the same
+// addresses conflict 2-way, so they go through lds_single.
+#ifndef MHPC_LDS_PITCH
+#define MHPC_LDS_PITCH 18
+#endif
+// (experiment: pitch 17 with the reads left to the compiler's ds_read2_b64 pairs, whose 16-lane
+// halves are conflict-free for an odd pitch)
+#ifndef MHPC_LDS_SINGLE
+#define MHPC_LDS_SINGLE (MHPC_LDS_PITCH % 2 == 0)
+#endif
+constexpr int MP = MHPC_LDS_PITCH;
+__device__ __forceinline__ constexpr int at(int r, int c) { return c * MP + r; }
+constexpr int kRowLdsPad = MP == 18 ? 1 : 3;  // 329 / 315 reals: adjacent problems' blocks on
+                                              // opposite bank halves
 struct RowLds {
-  alignas(16) real M[16 * MP];
-  real Gs[16];
-  real hx[14], Hs[9], h;
+  breal M[16 * MP];
+  breal Gs[16];
+  breal hx[14], Hs[9], h;
+  breal pad[kRowLdsPad];
 };
+static_assert(sizeof(RowLds) % (2 * sizeof(breal)) == sizeof(breal), "RowLds must stay an odd number of reals");
+
+typedef __attribute__((address_space(3))) const breal lds_creal;
+// Read p[j] of an LDS array as one single-word read: the pointer passes through an empty asm
+// first (no instruction), so the compiler cannot merge it with the neighbouring reads into a
+// ds_read2 / b128 (whose lane groups differ, see RowLds).  The caller threads the returned
+// pointer into the next read, so no copy of the address register is needed.
+__device__ __forceinline__ breal lds_single(lds_creal*& q, int j) {
+  if (MHPC_LDS_SINGLE) asm volatile("" : "+v"(q));
+  return q[j];
+}
 struct BwsLds {
   RowLds r[4];
 };
@@ -241,7 +348,7 @@ struct RowCtx {
   bool live;   // the row takes part in the current sweep attempt
   bool failed; // ... and its attempt has failed (PSD test) -- sticky for the attempt
   int nom;     // nominal trajectory slot
-  real reg;    // regularisation of the attempt
+  breal reg;    // regularisation of the attempt
   acc dV;      // expected cost change (row-uniform)
   int64_t kn, kn_wb, px_reads;
 };
@@ -252,7 +359,7 @@ __device__ __forceinline__ bool go(const RowCtx& r) { return r.live && !r.failed
 struct PendingKnot {
   bool ok;
   int k;
-  real K[4], du[4], G;
+  breal K[4], du[4], G;
 };
 __device__ __forceinline__ bool any_go(const RowCtx& r) {
   return __builtin_amdgcn_ballot_w64(go(r)) != 0;
@@ -265,6 +372,26 @@ __device__ __forceinline__ bool any_go(const RowCtx& r) {
 // Per knot the partials record (mhpc_solver.h: 18 columns x (7 qddot rows + 2 force rows),
 // then lu, luu, ly, lyy) is read straight into the lanes that own its columns; the next
 // knot's record is loaded while the current one computes.
+// Optional cycle accounting of the sweep (build with -DMHPC_BWS_TIMING, read with
+// mhpc_dbg_bws_cycles, tools/bws_timing.py; lane 0 of every wave): 0 / 1 WB knot loops and
+// knots, 2 / 3 SRB knot loops and knots, 4 terminal values, 5 impact steps, 6 kernel, 7 waves;
+// 8..12 the SRB knot's segments (operands and output stores issued; S and Q; the Qxx
+// transpose through LDS; the 4x4 control block: PSD test, factor, du, K, G; the value update
+// and the loop test).  Each probe is an s_memtime + wait, so the segments add up to more than
+// an uninstrumented knot (~250 cycles per probe) and LDS waits land in the segment that issued the
+// operations.
+#ifdef MHPC_BWS_TIMING
+__device__ unsigned long long g_bws_cyc[16];
+#define BWS_T(v) const unsigned long long v = threadIdx.x == 0 ? clock64() : 0ull
+#define BWS_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_bws_cyc[i], (unsigned long long)(v)); } while (0)
+// (segments accumulate per wave in registers, added to the counters once per phase: an atomic
+// per knot and segment from every wave serialised the timed loop behind the L2 atomics)
+#define BWS_SEG(i, a, b) BWS_T(b); segacc[(i) - 8] += (b) - (a)
+#else
+#define BWS_T(v) do { } while (0)
+#define BWS_ADD(i, v) do { } while (0)
+#define BWS_SEG(i, a, b) do { } while (0)
+#endif
 // knot iterations a sweep function ran: only the timing build keeps the count
 #ifdef MHPC_BWS_TIMING
 #define BWS_ITERS(n) (n)
@@ -279,28 +406,28 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
   using wk = wreal;
   const int t = rc.t, b = rc.b;
   const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
-  const real dt = L.dt[p];
+  const breal dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 14;
-  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
+  const breal coef = xl ? ((t & 1) ? dt : breal(1.0)) : breal(0.0);
   // identity part of W: W[r][c] = dt * rec + (c == 7 + r)
-  real base[7];
+  breal base[7];
 #pragma unroll
-  for (int r = 0; r < 7; ++r) base[r] = rho == 7 + r ? real(1.0) : real(0.0);
+  for (int r = 0; r < 7; ++r) base[r] = rho == 7 + r ? breal(1.0) : breal(0.0);
   // running-cost weight and fixed reference of state rho (CostBase.cpp:28-31)
   const int xi = xl ? rho : 0;
-  const real w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
-  const real rxc = xi == 1 ? sp.height : xi == 2 ? real(0.0)
-                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : real(0.0);
+  const breal w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
+  const breal rxc = xi == 1 ? sp.height : xi == 2 ? breal(0.0)
+                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : breal(0.0);
   // lxx + reg on the diagonal of Qxx (Ixx * regularisation): added twice to the transposed
   // copy in LDS, so that (Qxx + Qxx') / 2 carries it once
-  const real dg2 = xl ? 2 * (w2 + rc.reg) : real(0.0);
+  const breal dg2 = xl ? 2 * (w2 + rc.reg) : breal(0.0);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   // prefetch registers (record of one knot): the lane's own column of [Ac Bc; C D], the
   // second control column set (lanes 14, 15), one cost derivative per lane (broadcast below)
   constexpr int NR = STANCE ? 9 : 7;  // rows of a record column read
   constexpr int NCS = STANCE ? 14 : 8;  // cost derivatives (lu, luu [, ly, lyy])
-  real pr1[NR], pr2[NR], pcv, pxn, ppos;
+  breal pr1[NR], pr2[NR], pcv, pxn, ppos;
   const int c1 = rho;            // record column of W1 (0..15)
   const int c2 = 16 + (t & 1);   // second set: control columns 2, 3 (lanes 14, 15)
   const int cq = t < NCS ? t : 0;
@@ -322,11 +449,11 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr2[r] = r2[r];
   };
-  real H[14], Gv;
+  breal H[14], Gv;
   {
     const int hr = xl ? rho : 0;
 #pragma unroll
-    for (int j = 0; j < 14; ++j) H[j] = rl.M[hr * MP + j];
+    for (int j = 0; j < 14; ++j) H[j] = rl.M[at(hr, j)];
     Gv = rl.Gs[hr];
   }
   const int cr = rho;  // column of M read in the transpose (Qxu columns for lanes 14, 15)
@@ -358,15 +485,15 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
   for (int k = N - 2; k >= 0; --k) {
     ++it;
     // ---- the knot's derivatives (prefetched) ----
-    real W1[7], W2[7], G2o[2], G22[2];
+    breal W1[7], W2[7], G2o[2], G22[2];
 #pragma unroll
     for (int r = 0; r < 7; ++r) W1[r] = __builtin_fma(pr1[r], dt, base[r]);
 #pragma unroll
-    for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(pr2[r], dt, real(0.0));
+    for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(pr2[r], dt, breal(0.0));
     // C, D rows: copied out of the prefetch registers (a fresh value each, so the prefetch
     // buffer is dead before it is reloaded; a buffer live across its own reload costs a copy
     // at the back edge that waits for every outstanding memory operation, stores included)
-    G2o[0] = G2o[1] = G22[0] = G22[1] = real(0.0);
+    G2o[0] = G2o[1] = G22[0] = G22[1] = breal(0.0);
     if (STANCE) {
       asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
       asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
@@ -374,18 +501,18 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
       asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
     }
     // cost derivatives: lane q of the row holds entry q of (lu, luu, ly, lyy)
-    real luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
-    const real lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
+    breal luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
+    const breal lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
     luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
     if (STANCE) {
       ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
       lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
     }
-    const real rxi = rho == 0 ? ppos : rxc;
-    const real lx = w2 * (pxn - rxi);
-    const real lu01 = (t & 1) ? lu1 : lu0;
-    const real l1 = xl ? lx : lu01;
-    const real l2 = (t & 1) ? lu3 : lu2;
+    const breal rxi = rho == 0 ? ppos : rxc;
+    const breal lx = w2 * (pxn - rxi);
+    const breal lu01 = (t & 1) ? lu1 : lu0;
+    const breal l1 = xl ? lx : lu01;
+    const breal l2 = (t & 1) ? lu3 : lu2;
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     rc.kn_wb += gate ? 1 : 0;
@@ -403,14 +530,14 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
 
     // ---- S = H [A B] (lane: row rho of S) and Q = [A B]' S + ... (lane: row rho of Q),
     // column block by column block (a Q column needs only its S column) ----
-    real S[18], Q[18], Q2[2], Qv1, Qv2;
+    breal S[18], Q[18], Q2[2], Qv1, Qv2;
 #pragma unroll
     for (int c = 0; c < 7; ++c) S[c] = H[c];
 #pragma unroll
     for (int c = 7; c < 14; ++c) S[c] = dt * H[c - 7];
 #pragma unroll
-    for (int c = 14; c < 18; ++c) S[c] = real(0.0);
-    real cc[2] = {0, 0}, cc2[2] = {0, 0};
+    for (int c = 14; c < 18; ++c) S[c] = breal(0.0);
+    breal cc[2] = {0, 0}, cc2[2] = {0, 0};
     if (STANCE) {
       // C' lyy C etc.: cc[z] = sum_y G2[y][rho] lyy[y][z], then Q[.][d] += sum_z cc[z] G2[z][d]
 #pragma unroll
@@ -434,14 +561,14 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
 #pragma unroll
     for (int c = 12; c < 18; ++c) Q[c] = coef * qperm(S[c]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
-    Q2[0] = real(0.0);
-    Q2[1] = real(0.0);
+    Q2[0] = breal(0.0);
+    Q2[1] = breal(0.0);
     Qv2 = l2;
     {
-      const real sc[7] = {S[12], S[13], S[14], S[15], S[16], S[17], Gv};
+      const breal sc[7] = {S[12], S[13], S[14], S[15], S[16], S[17], Gv};
       sb_odd7_7(Q[12], Q[13], Q[14], Q[15], Q[16], Q[17], Qv1, sc, W1);
       // control rows 2, 3 (second set of lanes 14, 15): only their control columns
-      const real s2[3] = {S[16], S[17], Gv};
+      const breal s2[3] = {S[16], S[17], Gv};
       sb_odd7_3(Q2[0], Q2[1], Qv2, s2, W2);
     }
     if (STANCE) {
@@ -452,14 +579,17 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
 
     // ---- Qxx transpose through LDS (symmetrisation, MHPC_CompoundTypes.h:134) ----
 #pragma unroll
-    for (int j = 0; j < 16; ++j) rl.M[rho * MP + j] = Q[j];
+    for (int j = 0; j < 16; ++j) rl.M[at(rho, j)] = Q[j];
     // + 2 (lxx + reg) on the diagonal of the transposed copy: an LDS atomic add, in order with
     // this wave's other LDS operations, no round trip
-    atomicAdd(&rl.M[rho * MP + rho], dg2);
+    atomicAdd(&rl.M[at(rho, rho)], dg2);
     wave_lds_order();
-    real T[14];
+    breal T[14];
+    {
+      lds_creal* tq = (lds_creal*)&rl.M[at(0, cr)];
 #pragma unroll
-    for (int j = 0; j < 14; ++j) T[j] = rl.M[j * MP + cr];
+      for (int j = 0; j < 14; ++j) T[j] = lds_single(tq, j);
+    }
     wave_lds_order();
 
     // ---- the control block on every lane ----
@@ -476,15 +606,7 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
 #pragma unroll
       for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
     bool psd;
-    {
-      real A[16];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) A[a * 4 + c] = real(q[a][c]) - (a == c ? sp.eps9 : real(0.0));
-      psd = ldlt_nopiv_is_positive4(A);
-    }
-    const Ldl4<wk> F(q);
+    const Ldl4<wk> F = control_factor<wk>(q, sp.eps9, t, psd);
     // du = -Quu^-1 Qu, dV += -Qu' Quu^-1 Qu (no 1/2, MHPC_CompoundTypes.h:137-142)
     wk du[4], dv = wk(0.0);
     F.neg_solve(Qu, du);
@@ -506,8 +628,8 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
     wb_h_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Qxu, K);
     wb_h_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Qxu, K);
 #pragma unroll
-    for (int j = 0; j < 14; ++j) H[j] = real(Hn[j]);
-    Gv = real(Gn);
+    for (int j = 0; j < 14; ++j) H[j] = breal(Hn[j]);
+    Gv = breal(Gn);
     // ---- outputs of knot k (only while the row's attempt is alive) ----
     const bool ok = gate && psd;
     // outputs of knot k, stored at the top of the next knot (see store_pending)
@@ -515,10 +637,10 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      pend.K[a] = real(K[a]);
-      pend.du[a] = real(du[a]);
+      pend.K[a] = breal(K[a]);
+      pend.du[a] = breal(du[a]);
     }
-    pend.G = real(Gn);
+    pend.G = breal(Gn);
     if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
     if (!any_go(rc)) break;
@@ -528,7 +650,7 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
   __syncthreads();
   if (xl) {
 #pragma unroll
-    for (int j = 0; j < 14; ++j) rl.M[rho * MP + j] = H[j];
+    for (int j = 0; j < 14; ++j) rl.M[at(rho, j)] = H[j];
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
@@ -553,33 +675,31 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
   using wk = wreal;
   const int t = rc.t, b = rc.b, rp = rc.rp;
   const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
-  const real dt = L.dt[p];
+  const breal dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 14;
-  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
-  const real coefS = rp ? dt : real(1.0);  // S init: column s (row A) / 7 + s (row B)
+  const breal coef = xl ? ((t & 1) ? dt : breal(1.0)) : breal(0.0);
+  const breal coefS = rp ? dt : breal(1.0);  // S init: column s (row A) / 7 + s (row B)
   // broadcast column of the lane: its own (row A, odd lanes, lanes 14 / 15) or, on row B's
   // even lanes 2 s, the velocity column 7 + s
   const int cb = (rp && xl && !(t & 1)) ? 7 + (t >> 1) : rho;
-  real base[7], baseb[7];
+  breal base[7], baseb[7];
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
-    base[r] = rho == 7 + r ? real(1.0) : real(0.0);
-    baseb[r] = cb == 7 + r ? real(1.0) : real(0.0);
+    base[r] = rho == 7 + r ? breal(1.0) : breal(0.0);
+    baseb[r] = cb == 7 + r ? breal(1.0) : breal(0.0);
   }
   const int xi = xl ? rho : 0;
-  const real w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
-  const real rxc = xi == 1 ? sp.height : xi == 2 ? real(0.0)
-                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : real(0.0);
+  const breal w2 = 2 * dt * sp.cw.wQ[mode - 1][xi];
+  const breal rxc = xi == 1 ? sp.height : xi == 2 ? breal(0.0)
+                   : (xi >= 3 && xi < 7) ? cQjointBias[xi - 3] : xi == 7 ? sp.vel : breal(0.0);
   // lxx + reg on the diagonal, added by the row that owns the diagonal's column
   const bool own_diag = xl && ((rho < 7) == (rp == 0));
-  const real dg2 = own_diag ? 2 * (w2 + rc.reg) : real(0.0);
-  // LDS column of matrix column c (row B's half starts 16-byte aligned)
-  auto mcol = [](int c) { return c < 7 ? c : c + 1; };
+  const breal dg2 = own_diag ? 2 * (w2 + rc.reg) : breal(0.0);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   constexpr int NR = STANCE ? 9 : 7;
   constexpr int NCS = STANCE ? 14 : 8;
-  real pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;
+  breal pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;
   const int c2 = 16 + (t & 1);
   const int cq = t < NCS ? t : 0;
   // the phase's operand / output bases (knot 0): a knot adds k times its record stride
@@ -602,15 +722,18 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
 #pragma unroll
     for (int r = 0; r < NR; ++r) pr2[r] = r2[r];
   };
-  real H[14], Gv;
+  breal H[14], Gv;
   {
     const int hr = xl ? rho : 0;
 #pragma unroll
-    for (int j = 0; j < 14; ++j) H[j] = rl.M[hr * MP + j];
+    for (int j = 0; j < 14; ++j) H[j] = rl.M[at(hr, j)];
     Gv = rl.Gs[hr];
   }
-  const int cr = xl ? mcol(rho) : 0;   // LDS column read in the transpose
-  const int wo = rp ? 8 : 0;            // LDS column of the row's first Q column
+  // column read in the transpose; lanes 14, 15 (no row of Qxx) read column 0 with lane 0 (a
+  // broadcast): columns 14, 15 are never written in this layout, and a filler lane's H row
+  // still enters 0 * x products, so it must stay finite
+  const int cr = xl ? rho : 0;
+  const int wo = rp ? 7 : 0;            // column of the row's first Q slot
   const int jr = rp ? 7 : 0;            // first matrix row of the row's H columns
   PendingKnot pend;
   pend.ok = false;
@@ -635,14 +758,14 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
   int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
   for (int k = N - 2; k >= 0; --k) {
     ++it;
-    real Wo[7], Wb[7], W2[7], G2o[2], G2b[2], G22[2];
+    breal Wo[7], Wb[7], W2[7], G2o[2], G2b[2], G22[2];
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
       Wo[r] = __builtin_fma(pr1[r], dt, base[r]);
       Wb[r] = __builtin_fma(prb[r], dt, baseb[r]);
-      W2[r] = __builtin_fma(pr2[r], dt, real(0.0));
+      W2[r] = __builtin_fma(pr2[r], dt, breal(0.0));
     }
-    G2o[0] = G2o[1] = G2b[0] = G2b[1] = G22[0] = G22[1] = real(0.0);
+    G2o[0] = G2o[1] = G2b[0] = G2b[1] = G22[0] = G22[1] = breal(0.0);
     if (STANCE) {  // fresh values (see sweep_wb)
       asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
       asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
@@ -651,18 +774,18 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
       asm volatile("" : "=v"(G22[0]) : "0"(pr2[NR - 2]));
       asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
     }
-    real luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
-    const real lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
+    breal luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
+    const breal lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
     luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
     if (STANCE) {
       ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
       lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
     }
-    const real rxi = rho == 0 ? ppos : rxc;
-    const real lx = w2 * (pxn - rxi);
-    const real lu01 = (t & 1) ? lu1 : lu0;
-    const real l1 = xl ? lx : lu01;
-    const real l2 = (t & 1) ? lu3 : lu2;
+    const breal rxi = rho == 0 ? ppos : rxc;
+    const breal lx = w2 * (pxn - rxi);
+    const breal lu01 = (t & 1) ? lu1 : lu0;
+    const breal l1 = xl ? lx : lu01;
+    const breal l2 = (t & 1) ? lu3 : lu2;
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     rc.kn_wb += gate ? 1 : 0;
@@ -678,12 +801,12 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
     if (k > 0) load(k - 1);
 
     // ---- S and Q, slots 0..6 (the row's half of columns 0..13) and 7..10 (columns 14..17)
-    real S[11], Q[11], Q2[2], Qv1, Qv2;
+    breal S[11], Q[11], Q2[2], Qv1, Qv2;
 #pragma unroll
     for (int s = 0; s < 7; ++s) S[s] = coefS * H[s];
 #pragma unroll
-    for (int s = 7; s < 11; ++s) S[s] = real(0.0);
-    real cc[2] = {0, 0}, cc2[2] = {0, 0};
+    for (int s = 7; s < 11; ++s) S[s] = breal(0.0);
+    breal cc[2] = {0, 0}, cc2[2] = {0, 0};
     if (STANCE) {
 #pragma unroll
       for (int z = 0; z < 2; ++z) {
@@ -700,13 +823,13 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
 #pragma unroll
     for (int s = 6; s < 11; ++s) Q[s] = coef * qperm(S[s]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
-    Q2[0] = real(0.0);
-    Q2[1] = real(0.0);
+    Q2[0] = breal(0.0);
+    Q2[1] = breal(0.0);
     Qv2 = l2;
     {
-      const real sc[6] = {S[6], S[7], S[8], S[9], S[10], Gv};
+      const breal sc[6] = {S[6], S[7], S[8], S[9], S[10], Gv};
       sb_odd7_6(Q[6], Q[7], Q[8], Q[9], Q[10], Qv1, sc, Wo);
-      const real s2[3] = {S[9], S[10], Gv};
+      const breal s2[3] = {S[9], S[10], Gv};
       sb_odd7_3(Q2[0], Q2[1], Qv2, s2, W2);
     }
     if (STANCE) {
@@ -717,12 +840,15 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
 
     // ---- Qxx transpose: each row writes its half of the row rho ----
 #pragma unroll
-    for (int s = 0; s < 7; ++s) rl.M[rho * MP + wo + s] = Q[s];
-    atomicAdd(&rl.M[rho * MP + (xl ? mcol(rho) : rho)], dg2);
+    for (int s = 0; s < 7; ++s) rl.M[at(rho, wo + s)] = Q[s];
+    atomicAdd(&rl.M[at(rho, rho)], dg2);
     wave_lds_order();
-    real T[7];
+    breal T[7];
+    {
+      lds_creal* tq = (lds_creal*)&rl.M[at(jr, cr)];
 #pragma unroll
-    for (int s = 0; s < 7; ++s) T[s] = rl.M[(jr + s) * MP + cr];
+      for (int s = 0; s < 7; ++s) T[s] = lds_single(tq, s);
+    }
     wave_lds_order();
 
     // ---- the control block on every lane (both rows alike) ----
@@ -738,15 +864,7 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
 #pragma unroll
       for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
     bool psd;
-    {
-      real A[16];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) A[a * 4 + c] = real(q[a][c]) - (a == c ? sp.eps9 : real(0.0));
-      psd = ldlt_nopiv_is_positive4(A);
-    }
-    const Ldl4<wk> F(q);
+    const Ldl4<wk> F = control_factor<wk>(q, sp.eps9, t, psd);
     wk du[4], dv = wk(0.0);
     F.neg_solve(Qu, du);
 #pragma unroll
@@ -768,17 +886,17 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
     wb_h_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], QxuS, K);
     // both rows get both halves
 #pragma unroll
-    for (int s = 0; s < 7; ++s) row_pair_swap(real(Hn[s]), H[s], H[7 + s]);
-    Gv = real(Gn);
+    for (int s = 0; s < 7; ++s) row_pair_swap(breal(Hn[s]), H[s], H[7 + s]);
+    Gv = breal(Gn);
     const bool ok = gate && psd;
     pend.ok = ok && rp == 0;
     pend.k = k;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      pend.K[a] = real(K[a]);
-      pend.du[a] = real(du[a]);
+      pend.K[a] = breal(K[a]);
+      pend.du[a] = breal(du[a]);
     }
-    pend.G = real(Gn);
+    pend.G = breal(Gn);
     if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
     if (!any_go(rc)) break;
@@ -787,7 +905,7 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
   __syncthreads();
   if (xl && rp == 0) {
 #pragma unroll
-    for (int j = 0; j < 14; ++j) rl.M[rho * MP + j] = H[j];
+    for (int j = 0; j < 14; ++j) rl.M[at(rho, j)] = H[j];
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
@@ -795,18 +913,18 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
 }
 
 // SRB Jacobian entry of row 3+r, column col of [A B] (FBDynamics_par.c operation order).
-__device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const real* u,
-                                              const real* p, const real* s, real dt) {
+__device__ __forceinline__ breal srb_w_entry(int r, int col, const breal* x, const breal* u,
+                                              const breal* p, const breal* s, breal dt) {
   MHPC_NO_FMA
   const int row = 3 + r;
-  real ac = real(0.0);
+  breal ac = breal(0.0);
   if (col < 6) {
     if (row == 5 && col == 0) ac = s[0] * (kSrbInvInertia * u[1]) + s[1] * (kSrbInvInertia * u[3]);
     if (row == 5 && col == 1) ac = -(s[0] * (kSrbInvInertia * u[0]) + s[1] * (kSrbInvInertia * u[2]));
-    return (col == row ? real(1.0) : real(0.0)) + ac * dt;
+    return (col == row ? breal(1.0) : breal(0.0)) + ac * dt;
   }
   const int c = col - 6;
-  real bc = real(0.0);
+  breal bc = breal(0.0);
   if (row == 3 && c == 0) bc = kSrbInvMass * s[0];
   if (row == 5 && c == 0) bc = s[0] * (kSrbInvInertia * (p[1] - x[1]));
   if (row == 4 && c == 1) bc = kSrbInvMass * s[0];
@@ -820,23 +938,23 @@ __device__ __forceinline__ real srb_w_entry(int r, int col, const real* x, const
 
 // Row 5 (theta) of W, column col, from the lane's two knot operands (srb_w_entry(2, ...) term
 // for term): e0, e1 = u1, u3 (col 0) / u0, u2 (col 1); e0 = z (cols 6, 8) / x (cols 7, 9).
-__device__ __forceinline__ real srb_w2_lane(int col, real e0, real e1, const real* p, const real* s,
-                                            real dt) {
+__device__ __forceinline__ breal srb_w2_lane(int col, breal e0, breal e1, const breal* p, const breal* s,
+                                            breal dt) {
   MHPC_NO_FMA
   // every candidate term, then selects (no divergent branches in the knot loop)
   const int c = col - 6;
   // (values first, then selects: a select between addresses of the caller's array would
   // keep that array in scratch)
-  const real f0 = p[0], f1 = p[1], f2 = p[2], f3 = p[3], s0 = s[0], s1 = s[1];
-  real pp = f2;
+  const breal f0 = p[0], f1 = p[1], f2 = p[2], f3 = p[3], s0 = s[0], s1 = s[1];
+  breal pp = f2;
   pp = c == 2 ? f3 : pp;
   pp = c == 1 ? f0 : pp;
   pp = c == 0 ? f1 : pp;
-  const real bs = (c < 2 ? s0 : s1) * (kSrbInvInertia * (pp - e0));
-  const real ia = s0 * (kSrbInvInertia * e0) + s1 * (kSrbInvInertia * e1);
-  const real ac = col == 0 ? ia : col == 1 ? -ia : real(0.0);
-  const real bc = (c & 1) ? -bs : bs;
-  return col < 6 ? (col == 5 ? real(1.0) : real(0.0)) + ac * dt : bc * dt;
+  const breal bs = (c < 2 ? s0 : s1) * (kSrbInvInertia * (pp - e0));
+  const breal ia = s0 * (kSrbInvInertia * e0) + s1 * (kSrbInvInertia * e1);
+  const breal ac = col == 0 ? ia : col == 1 ? -ia : breal(0.0);
+  const breal bc = (c & 1) ? -bs : bs;
+  return col < 6 ? (col == 5 ? breal(1.0) : breal(0.0)) + ac * dt : bc * dt;
 }
 // Knot-record offsets of a lane's two W-row-5 operands (see srb_w2_lane)
 __device__ __forceinline__ int srb_w2_off(int col, int which) {
@@ -867,39 +985,47 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
   using R = Rows<3>;
   const int t = rc.t, b = rc.b;
   const int N = L.N[p], ko = L.ko[p], mode = L.mode[p];
-  const real dt = L.dt[p];
+  const breal dt = L.dt[p];
   const int rho = R::rho(t);
   const bool xl = t < 6;
   const int cj = rho < 10 ? rho : 0;  // column of [A B] held (clamped for spare lanes)
-  const real coef = xl ? ((t & 1) ? dt : real(1.0)) : real(0.0);
-  real foot[4], cs[2];
-  plan_foothold(traj_ptr(sp, d, b, rc.nom, ko), dt * N, mode, foot);
-  srb_contact(mode, cs);
+  const breal coef = xl ? ((t & 1) ? dt : breal(1.0)) : breal(0.0);
+  // foothold and contact flags in the model's type, as the line search planned them
+  breal foot[4], cs[2];
+  {
+    real fr[4], cr2[2];
+    plan_foothold(traj_ptr(sp, d, b, rc.nom, ko), L.dt[p] * N, mode, fr);
+    srb_contact(mode, cr2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) foot[i] = fr[i];
+    cs[0] = cr2[0];
+    cs[1] = cr2[1];
+  }
   const int m = mode - 1;
   // per-lane cost weight 2 dt Q / 2 dt R and fixed reference of row cj
-  real w2, rxc;
+  breal w2, rxc;
   if (cj < 6) {
     w2 = 2 * dt * sp.cw.fQ[m][cj];
-    rxc = cj == 1 ? sp.height : cj == 3 ? sp.vel : real(0.0);
+    rxc = cj == 1 ? sp.height : cj == 3 ? sp.vel : breal(0.0);
   } else {
     const int c = cj - 6;
     w2 = 2 * dt * sp.cw.fR[m][c];
-    rxc = (c == 1 || c == 3) ? real(8.252) * real(9.81) : real(0.0);
+    rxc = (c == 1 || c == 3) ? breal(8.252) * breal(9.81) : breal(0.0);
   }
-  real luu[4];
+  breal luu[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) luu[c] = 2 * dt * sp.cw.fR[m][c];
   // lxx + reg, see sweep_wb (two-row layout: both rows run this phase, row A adds)
-  const real dg2 = xl && rc.rp == 0 ? 2 * (w2 + rc.reg) : real(0.0);
+  const breal dg2 = xl && rc.rp == 0 ? 2 * (w2 + rc.reg) : breal(0.0);
   // rows 3, 4 of W do not depend on the knot
-  const real zx[2] = {0, 0}, zu[4] = {0, 0, 0, 0};
-  const real W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
-  const real W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
+  const breal zx[2] = {0, 0}, zu[4] = {0, 0, 0, 0};
+  const breal W0c = srb_w_entry(0, cj, zx, zu, foot, cs, dt);
+  const breal W1c = srb_w_entry(1, cj, zx, zu, foot, cs, dt);
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   // a lane's knot operands from the nominal: its two W-row-5 operands (or x, z, u), its own
   // entry, the position reference
   struct Ops {
-    real e0, e1, v, pos, xs[2], us[4];
+    breal e0, e1, v, pos, xs[2], us[4];
   };
   const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko);  // knot k adds k KS
   const int oe0 = srb_w2_off(cj, 0), oe1 = srb_w2_off(cj, 1);
@@ -916,11 +1042,11 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
       for (int c = 0; c < 4; ++c) o.us[c] = tk[6 + c];
     }
   };
-  real H[6], Gv;
+  breal H[6], Gv;
   {
     const int hr = xl ? rho : 0;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) H[j] = rl.M[hr * MP + j];
+    for (int j = 0; j < 6; ++j) H[j] = rl.M[at(hr, j)];
     Gv = rl.Gs[hr];
   }
   const int cr = rho < 10 ? rho : 0;
@@ -944,6 +1070,9 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     pend.ok = false;
   };
   Ops oa, ob;
+#ifdef MHPC_BWS_TIMING
+  unsigned long long segacc[5] = {0, 0, 0, 0, 0};
+#endif
   if (N >= 2) load(N - 2, oa);
   if (SRB_PF > 1 && N >= 3) load(N - 3, ob);
   int it = 0;  // knot iterations the wave ran (the cycle accounting's knot count)
@@ -951,13 +1080,14 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
   // of the wave goes on
   auto knot = [&](int k, Ops& o) __attribute__((always_inline)) {
     ++it;
-    real W[3];
+    BWS_T(sg0);
+    breal W[3];
     W[0] = W0c;
     W[1] = W1c;
     W[2] = LANE_OPS ? srb_w2_lane(cj, o.e0, o.e1, foot, cs, dt)
                     : srb_w_entry(2, cj, o.xs, o.us, foot, cs, dt);
-    const real rxi = rho == 0 ? o.pos : rxc;
-    const real l1 = w2 * (o.v - rxi);
+    const breal rxi = rho == 0 ? o.pos : rxc;
+    const breal l1 = w2 * (o.v - rxi);
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     asm volatile("" ::"v"(W[2]), "v"(l1));  // see sweep_wb
@@ -966,16 +1096,17 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     if (SRB_PF > 1 && k >= SRB_PF) load(k - SRB_PF, o);
     store_pending();
     if (SRB_PF == 1 && k > 0) load(k - 1, o);
-    real S[10];
+    BWS_SEG(8, sg0, sg1);
+    breal S[10];
 #pragma unroll
     for (int c = 0; c < 3; ++c) S[c] = H[c];
 #pragma unroll
     for (int c = 3; c < 6; ++c) S[c] = dt * H[c - 3];
 #pragma unroll
-    for (int c = 6; c < 10; ++c) S[c] = real(0.0);
+    for (int c = 6; c < 10; ++c) S[c] = breal(0.0);
     // (only the structurally non-zero W terms: W is 5 + 8 non-zeros, FBDynamics_par.c:53-54)
     srb_sp_a(S[0], S[1], S[3], S[4], W, H + 3);
-    real Q[10], Qv1;
+    breal Q[10], Qv1;
 #pragma unroll
     for (int c = 0; c < 5; ++c) Q[c] = coef * qperm(S[c]);
     sb_odd3_5(Q[0], Q[1], Q[2], Q[3], Q[4], S + 0, W);
@@ -984,18 +1115,23 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     for (int c = 5; c < 10; ++c) Q[c] = coef * qperm(S[c]);
     Qv1 = __builtin_fma(coef, qperm(Gv), l1);
     {
-      const real sc[6] = {S[5], S[6], S[7], S[8], S[9], Gv};
+      const breal sc[6] = {S[5], S[6], S[7], S[8], S[9], Gv};
       sb_odd3_6(Q[5], Q[6], Q[7], Q[8], Q[9], Qv1, sc, W);
     }
+    BWS_SEG(9, sg1, sg2);
 #pragma unroll
-    for (int j = 0; j < 10; ++j) rl.M[(rho & 15) * MP + j] = Q[j];
-    atomicAdd(&rl.M[(rho & 15) * MP + (rho & 15)], dg2);  // see sweep_wb
+    for (int j = 0; j < 10; ++j) rl.M[at(rho & 15, j)] = Q[j];
+    atomicAdd(&rl.M[at(rho & 15, rho & 15)], dg2);  // see sweep_wb
     wave_lds_order();
-    real T[6];
+    breal T[6];
+    {
+      lds_creal* tq = (lds_creal*)&rl.M[at(0, cr)];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) T[j] = rl.M[j * MP + cr];
+      for (int j = 0; j < 6; ++j) T[j] = lds_single(tq, j);
+    }
     wave_lds_order();
-    real q[4][4], Qu[4];
+    BWS_SEG(10, sg2, sg3);
+    breal q[4][4], Qu[4];
     q[0][0] = rbc<6>(Q[6]); q[0][1] = rbc<6>(Q[7]); q[0][2] = rbc<6>(Q[8]); q[0][3] = rbc<6>(Q[9]);
     q[1][1] = rbc<7>(Q[7]); q[1][2] = rbc<7>(Q[8]); q[1][3] = rbc<7>(Q[9]);
     q[2][2] = rbc<8>(Q[8]); q[2][3] = rbc<8>(Q[9]); q[3][3] = rbc<9>(Q[9]);
@@ -1007,27 +1143,20 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
 #pragma unroll
       for (int c = 0; c < a; ++c) q[a][c] = q[c][a];
     bool psd;
-    {
-      real A[16];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) A[a * 4 + c] = q[a][c] - (a == c ? sp.eps9 : real(0.0));
-      psd = ldlt_nopiv_is_positive4(A);
-    }
-    const Ldl4<real> F(q);
-    real du[4], dv = real(0.0);
+    const Ldl4<breal> F = control_factor<breal>(q, sp.eps9, t, psd);
+    breal du[4], dv = breal(0.0);
     F.neg_solve(Qu, du);
 #pragma unroll
     for (int a = 0; a < 4; ++a) dv += Qu[a] * du[a];
-    real Qxu[4], K[4];
+    breal Qxu[4], K[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) Qxu[c] = Q[6 + c];
     F.neg_solve(Qxu, K);
-    real Gn = Qv1;
+    breal Gn = Qv1;
 #pragma unroll
     for (int a = 0; a < 4; ++a) Gn += K[a] * Qu[a];
-    real Hn[6];
+    BWS_SEG(11, sg3, sg4);
+    breal Hn[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) Hn[j] = (Q[j] + T[j]) / 2;
     srb_h(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Qxu, K);
@@ -1045,7 +1174,9 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     pend.G = Gn;
     if (ok) rc.dV += acc(dv);
     rc.failed = rc.failed || (gate && !psd);
-    return any_go(rc);
+    const bool more = any_go(rc);
+    BWS_SEG(12, sg4, sg5);
+    return more;
   };
   if (SRB_PF == 1) {
     for (int k = N - 2; k >= 0; --k)
@@ -1058,10 +1189,13 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     }
   }
   store_pending();
+#ifdef MHPC_BWS_TIMING
+  for (int i = 0; i < 5; ++i) BWS_ADD(8 + i, segacc[i]);
+#endif
   __syncthreads();
   if (xl) {
 #pragma unroll
-    for (int j = 0; j < 6; ++j) rl.M[rho * MP + j] = H[j];
+    for (int j = 0; j < 6; ++j) rl.M[at(rho, j)] = H[j];
     rl.Gs[rho] = Gv;
   }
   __syncthreads();
@@ -1077,11 +1211,11 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const La
                                RowLds& rl, const RowCtx& rc, int p) {
   constexpr bool wb = NX == 14;
   const int mode = L.mode[p], N = L.N[p], ko = L.ko[p];
-  const real pos = d.refpos[(size_t)rc.b * sp.NK + ko + N - 1];
+  const breal pos = d.refpos[(size_t)rc.b * sp.NK + ko + N - 1];
   const real* xe = traj_ptr(sp, d, rc.b, rc.nom, ko + N - 1);
   const bool al = wb && ntc_of(mode, true) && sp.AL_active && st->al_partials;
   if (al && rc.lt == 0) {
-    real hx[14], Hs[3][3], h;
+    real hx[14], Hs[3][3], h;  // (the model's type)
     if (mode == 2) wb_touchdown_compact<kFront>(xe, &h, hx, Hs);
     else wb_touchdown_compact<kBack>(xe, &h, hx, Hs);
 #pragma unroll
@@ -1091,8 +1225,8 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const La
     rl.h = h;
   }
   __syncthreads();
-  const real h = al ? rl.h : real(0.0);
-  const real s = st->sigma[p], lam = st->lambda[p];
+  const breal h = al ? rl.h : breal(0.0);
+  const breal s = st->sigma[p], lam = st->lambda[p];
   const int ih = mode == 2 ? 3 : 5;  // touchdown Hessian block (theta, hip, knee)
   real* Gout = d.G + ((size_t)rc.b * sp.NK + ko + N - 1) * 14;
   const bool gate = go(rc);
@@ -1100,22 +1234,22 @@ __device__ void terminal_value(const SolveParams& sp, const DevBufs& d, const La
   for (int e = rc.lt; e < NX * NX + NX; e += rc.nl) {
     if (e < NX * NX) {
       const int i = e / NX, j = e - i * NX;
-      real v = i == j ? (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) : real(0.0);
+      breal v = i == j ? (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) : breal(0.0);
       if (al) {
         const int ai = i == 2 ? 0 : (i == ih ? 1 : (i == ih + 1 ? 2 : -1));
         const int aj = j == 2 ? 0 : (j == ih ? 1 : (j == ih + 1 ? 2 : -1));
-        const real hij = (ai >= 0 && aj >= 0) ? rl.Hs[ai * 3 + aj] : real(0.0);
+        const breal hij = (ai >= 0 && aj >= 0) ? rl.Hs[ai * 3 + aj] : breal(0.0);
         v += 50 * (s * s / 2 * (rl.hx[i] * rl.hx[j] + h * hij) + lam * hij);
       }
-      rl.M[i * MP + j] = v + rl.M[i * MP + j];
+      rl.M[at(i, j)] = v + rl.M[at(i, j)];
     } else {
       const int i = e - NX * NX;
-      real rxi;
+      breal rxi;
       if (wb) rxi = i == 0 ? pos : (i == 7 ? sp.vel : cXtermWB[mode - 1][i]);
-      else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : real(0.0)));
-      real v = (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) * (xe[i] - rxi);
+      else rxi = i == 0 ? pos : (i == 1 ? sp.height : (i == 3 ? sp.vel : breal(0.0)));
+      breal v = (wb ? sp.cw.wQf[mode - 1][i] : sp.cw.fQf[mode - 1][i]) * (xe[i] - rxi);
       if (al) v += 50 * (s * s / 2 * rl.hx[i] * h + lam * rl.hx[i]);
-      const real g = v + rl.Gs[i];
+      const breal g = v + rl.Gs[i];
       rl.Gs[i] = g;
       if (gate) Gout[i] = g;
     }
@@ -1133,33 +1267,33 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, const Layou
   const bool imp = mode == 2 || mode == 4;
   const int i = t < 14 ? R::rho(t) : 0;
   // lift to the full-model space: E' G', E' H' E (E = _stateProj for an SRB next phase)
-  real H2[14], G2v;
+  breal H2[14], G2v;
   {
     const int pi = nwb ? i : (i < 3 ? i : (i >= 7 && i < 10 ? i - 4 : -1));
     const int pr = pi >= 0 ? pi : 0;
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
       const int pj = nwb ? j : (j < 3 ? j : (j >= 7 && j < 10 ? j - 4 : -1));
-      const real v = pj >= 0 ? rl.M[pr * MP + pj] : real(0.0);
-      H2[j] = pi >= 0 ? v : real(0.0);
+      const breal v = pj >= 0 ? rl.M[at(pr, pj)] : breal(0.0);
+      H2[j] = pi >= 0 ? v : breal(0.0);
     }
-    G2v = pi >= 0 ? rl.Gs[pr] : real(0.0);
+    G2v = pi >= 0 ? rl.Gs[pr] : breal(0.0);
   }
-  real Hn[14], Gn;
+  breal Hn[14], Gn;
   if (imp) {
     // Px column i (column-major record): Pc[m] = Px[m][i]
     const real* pxc = d.px + ((size_t)rc.b * MAXP + p) * 196 + i * 14;
-    real Pc[14];
+    breal Pc[14];
 #pragma unroll
     for (int m = 0; m < 14; ++m) Pc[m] = pxc[m];
     if (go(rc) && t == 0) ++rc.px_reads;
     // T = Px' H2 (lane: row i), G = Px' G2: sum over m = 0..13 in order
-    real T[14];
+    breal T[14];
 #pragma unroll
-    for (int j = 0; j < 14; ++j) T[j] = real(0.0);
-    Gn = real(0.0);
+    for (int j = 0; j < 14; ++j) T[j] = breal(0.0);
+    Gn = breal(0.0);
     {
-      const real h2b[8] = {H2[7], H2[8], H2[9], H2[10], H2[11], H2[12], H2[13], G2v};
+      const breal h2b[8] = {H2[7], H2[8], H2[9], H2[10], H2[11], H2[12], H2[13], G2v};
       sb_even7_7(T[0], T[1], T[2], T[3], T[4], T[5], T[6], H2, Pc);
       sb_even7_8(T[7], T[8], T[9], T[10], T[11], T[12], T[13], Gn, h2b, Pc);
       sb_odd7_7(T[0], T[1], T[2], T[3], T[4], T[5], T[6], H2, Pc + 7);
@@ -1167,7 +1301,7 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, const Layou
     }
     // H = T Px: H[i][j] = sum_m T[i][m] Px[m][j], Px[m][j] on lane lam(j)
 #pragma unroll
-    for (int j = 0; j < 14; ++j) Hn[j] = real(0.0);
+    for (int j = 0; j < 14; ++j) Hn[j] = breal(0.0);
     wb_p_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Pc, T);
     wb_p_b(Hn[7], Hn[8], Hn[9], Hn[10], Hn[11], Hn[12], Hn[13], Pc, T);
     wb_p_a(Hn[0], Hn[1], Hn[2], Hn[3], Hn[4], Hn[5], Hn[6], Pc + 7, T + 7);
@@ -1180,23 +1314,12 @@ __device__ void impact_step(const SolveParams& sp, const DevBufs& d, const Layou
   __syncthreads();
   if (t < 14) {
 #pragma unroll
-    for (int j = 0; j < 14; ++j) rl.M[i * MP + j] = Hn[j];
+    for (int j = 0; j < 14; ++j) rl.M[at(i, j)] = Hn[j];
     rl.Gs[i] = Gn;
   }
   __syncthreads();
 }
 
-// Optional cycle accounting of the sweep (build with -DMHPC_BWS_TIMING, read with
-// mhpc_dbg_bws_cycles, tools/bws_timing.py; lane 0 of every wave): 0 / 1 WB knot loops and
-// knots, 2 / 3 SRB knot loops and knots, 4 terminal values, 5 impact steps, 6 kernel, 7 waves.
-#ifdef MHPC_BWS_TIMING
-__device__ unsigned long long g_bws_cyc[8];
-#define BWS_T(v) const unsigned long long v = threadIdx.x == 0 ? clock64() : 0ull
-#define BWS_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_bws_cyc[i], (unsigned long long)(v)); } while (0)
-#else
-#define BWS_T(v) do { } while (0)
-#define BWS_ADD(i, v) do { } while (0)
-#endif
 
 // One sweep attempt over phases p_hi..p_lo (MultiPhaseDDP::backward_sweep).  On entry
 // rl.M / rl.Gs hold the value function entering phase p_hi (zero for the last phase) and
@@ -1257,8 +1380,8 @@ __device__ void sweep_phases(const SolveParams& sp, const DevBufs& d, const Layo
 __device__ void zero_value(RowLds& rl, RowCtx& rc) {
   __syncthreads();
   #pragma unroll 1
-  for (int e = rc.lt; e < 16 * MP; e += rc.nl) rl.M[e] = real(0.0);
-  if (rc.lt < 16) rl.Gs[rc.lt] = real(0.0);
+  for (int e = rc.lt; e < 16 * MP; e += rc.nl) rl.M[e] = breal(0.0);
+  if (rc.lt < 16) rl.Gs[rc.lt] = breal(0.0);
   rc.dV = acc(0.0);
   __syncthreads();
 }
@@ -1324,12 +1447,12 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       __syncthreads();
       if (rc.live && !rc.failed) {  // (now: a later attempt of another row reuses rl)
         #pragma unroll 1
-        for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[(e / 6) * MP + e % 6];
+        for (int e = rc.t; e < 36; e += 16) c.H[e] = rl.M[at(e / 6, e % 6)];
         if (rc.t < 6) c.G[rc.t] = rl.Gs[rc.t];
       }
       pending = rc.live && rc.failed;
       if (pending) {  // the next attempt, as PART 0 would start it
-        rc.reg = fmax(rc.reg * update_reg, real(1e-03));
+        rc.reg = fmax(rc.reg * update_reg, breal(1e-03));
         ++bws_iter;
         if (rc.reg > 1000) {
           aborted = true;
@@ -1354,7 +1477,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
       const BwsCarry& c = d.carry[rc.b];
       __syncthreads();
       #pragma unroll 1
-      for (int e = rc.lt; e < 36; e += rc.nl) rl.M[(e / 6) * MP + e % 6] = c.H[e];
+      for (int e = rc.lt; e < 36; e += rc.nl) rl.M[at(e / 6, e % 6)] = c.H[e];
       if (rc.lt < 6) rl.Gs[rc.lt] = c.G[rc.lt];
       __syncthreads();
       if (rc.live) {
@@ -1373,7 +1496,7 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
     }
     pending = rc.live && rc.failed && !aborted;
     if (pending) {
-      rc.reg = fmax(rc.reg * update_reg, real(1e-03));  // MultiPhaseDDP.cpp:218
+      rc.reg = fmax(rc.reg * update_reg, breal(1e-03));  // MultiPhaseDDP.cpp:218
       ++bws_iter;
       if (rc.reg > 1000) {
         aborted = true;
@@ -1402,8 +1525,8 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
                                   (bws_iter & 0xff);
     } else {
       st->dV_exp = st->dV[0];  // _exp_cost_change = _phases[0]->_dV
-      real reg = rc.reg / 20;  // MultiPhaseDDP.cpp:237-241
-      if (reg < real(1e-06)) reg = 0;
+      breal reg = rc.reg / 20;  // MultiPhaseDDP.cpp:237-241
+      if (reg < breal(1e-06)) reg = 0;
       st->reg = reg;
     }
   }
@@ -1465,11 +1588,11 @@ bool bws_split(const SolveParams& sp) {
 #ifdef MHPC_BWS_TIMING
 extern "C" int mhpc_dbg_bws_cycles(unsigned long long* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_bws_cyc), sizeof(unsigned long long) * 8) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(MHPC_NS::g_bws_cyc), sizeof(unsigned long long) * 16) !=
       hipSuccess)
     return 1;
   if (reset) {
-    unsigned long long z[8] = {0};
+    unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(MHPC_NS::g_bws_cyc), z, sizeof(z)) != hipSuccess) return 1;
   }
   return 0;

@@ -1832,6 +1832,10 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
     if (e == hipSuccess) e = hipStreamWaitEvent(s3, fork, 0);
     if (e != hipSuccess) return e;
   }
+#ifdef MHPC_PAR_IMPACT_FIRST  // experiment: the impact Jacobians ahead of the second group
+  if (ti > 0)
+    hipLaunchKernelGGL(k_partials_impact, dim3(ti), dim3(256), 0, two ? s3 : s, sp, d);
+#endif
   if (tk > 0) {
     constexpr int nt = MHPC_PAR_BLOCK;
     const dim3 grid(tk);
@@ -1842,9 +1846,11 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
       hipLaunchKernelGGL(k_partials<3>, grid, dim3(nt), 0, s, sp, d);
     }
   }
+#ifndef MHPC_PAR_IMPACT_FIRST
   if (ti > 0)
     hipLaunchKernelGGL(k_partials_impact, dim3(ti), dim3(256), 0, two ? s3 : s,
                        sp, d);
+#endif
   if (two) {
     hipError_t e = hipEventRecord(join, s3);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);

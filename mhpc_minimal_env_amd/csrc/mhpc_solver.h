@@ -166,10 +166,10 @@ struct ProbState {
 // SRB part passed the PSD test -- the SRB half retries attempts that fail there itself --,
 // that attempt's regularisation and number (bws_iter), whether the retries aborted
 // (regularisation > 1000), the attempts and SRB knots swept.
-struct BwsCarry {
-  real H[196];
-  real G[14];
-  real reg;
+struct BwsCarry {  // double in both builds: the sweep's arithmetic type (mhpc_bws.hip breal)
+  double H[196];
+  double G[14];
+  double reg;
   int32_t abort, iter, sweeps, knots;
 };
 

@@ -17,7 +17,7 @@ desc = configs.c3_desc()
 loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=B, device=0)
 loco.set_kernel_variant(bws=var)
 loco.set_initial_condition(configs.x0_for(desc, B))
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 for it in range(2):
     loco.initialization()
     dbg(buf, 1)
@@ -31,3 +31,8 @@ print(f"  WB knots      {c[0] / waves:10.0f} cyc  {c[1] / waves:6.1f} knots  {c[
 print(f"  SRB knots     {c[2] / waves:10.0f} cyc  {c[3] / waves:6.1f} knots  {c[2] / max(c[3], 1):7.0f} cyc/knot")
 print(f"  terminal      {c[4] / waves:10.0f} cyc")
 print(f"  impact        {c[5] / waves:10.0f} cyc")
+nk = max(c[3], 1)
+segs = ("operands / stores", "S and Q", "Qxx transpose (LDS)", "control block", "value update")
+print("  SRB knot segments (instrumented, per knot):")
+for i, name in enumerate(segs):
+    print(f"    {name:22s} {c[8 + i] / nk:7.0f} cyc")
