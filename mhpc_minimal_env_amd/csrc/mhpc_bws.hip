@@ -256,7 +256,7 @@ struct Ldl4 {
 // never stored or broadcast.  MHPC_BWS_PSD_SEPARATE=1: the test as its own factorisation (the
 // round-5 form; same verdicts and factors bit for bit, tests/test_gpu_variants.py).
 #ifndef MHPC_BWS_PSD_SEPARATE
-#define MHPC_BWS_PSD_SEPARATE 0
+#define MHPC_BWS_PSD_SEPARATE 1
 #endif
 template <class W>
 __device__ __forceinline__ Ldl4<W> control_factor(const W (&q)[4][4], breal eps9, int t, bool& psd) {

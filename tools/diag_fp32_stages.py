@@ -13,6 +13,7 @@ import oracle as O  # noqa: E402
 from mhpc_minimal_env_amd import configs, locomotion as L  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+WATCH = int(sys.argv[2]) if len(sys.argv) > 2 else -1  # one problem to report per phase
 desc = configs.c5_desc(32)
 d64 = configs.c5_desc(64)
 x0 = configs.x0_for(desc, B)
@@ -43,11 +44,15 @@ for name, al, ddp, solve in (("warm start", 2, 3, False), ("AL1 x DDP1", 1, 1, T
     ref = O.solve(d64, opt.to_c(), x0, nthreads=8, do_solve=solve)
     gx, rx = split(g["X"], desc.xsize), split(ref["X"], desc.xsize)
     gk, rk = split(g["K"], lambda p: 4 * desc.xsize(p)), split(ref["K"], lambda p: 4 * desc.xsize(p))
+    gg, rg = split(g["G"], desc.xsize), split(ref["G"], desc.xsize)
     same = (sc["trace"] == ref["trace"]).all(axis=1).mean() if solve else 1.0
     rel = np.abs(sc["J"] - ref["J"]) / np.abs(ref["J"]) if solve else np.zeros(B)
     print(f"== {name}: traces {same:.3f}, J rel err median {np.median(rel):.1e} max {rel.max():.1e}")
     for p in range(P):
         dx = np.max(np.abs(gx[p] - rx[p]), axis=1)
         kr = np.max(np.abs(gk[p] - rk[p]), axis=1) / np.maximum(1e-30, np.max(np.abs(rk[p]), axis=1))
+        gr = np.max(np.abs(gg[p] - rg[p]), axis=1) / np.maximum(1.0, np.max(np.abs(rg[p]), axis=1))
+        w = (f"   problem {WATCH}: dx {dx[WATCH]:.1e} K {kr[WATCH]:.1e} G {gr[WATCH]:.1e} "
+             f"(|G|max {np.abs(rg[p][WATCH]).max():.1e})") if WATCH >= 0 else ""
         print(f"   phase {p}: max|dx| median {np.median(dx):.1e} worst {dx.max():.1e}   "
-              f"K rel median {np.median(kr):.1e} worst {kr.max():.1e}")
+              f"K rel median {np.median(kr):.1e} worst {kr.max():.1e}   G worst {gr.max():.1e}" + w)
