@@ -270,7 +270,8 @@ def workload_text(name: str) -> str:
 class Solver:
     """One handle on this rank's GPU, stepping init + solve of its batch."""
 
-    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0, 0), layouts=None):
+    def __init__(self, desc, opt, x0, device, variants=("auto", "auto", "auto", 0, 0), layouts=None,
+                 sweep_bits=0):
         from mhpc_minimal_env_amd import capi
         from mhpc_minimal_env_amd import locomotion as L
         self.capi = capi
@@ -278,7 +279,8 @@ class Solver:
         if layouts is not None:  # per-problem phase layouts (gait schedules)
             self.loco.set_layouts(*layouts)
         self.loco.set_kernel_variant(bws=variants[0], rollout=variants[1], overlap=variants[2],
-                                     sub_batches=variants[3], ro_store=variants[4])
+                                     sub_batches=variants[3], ro_store=variants[4],
+                                     sweep_bits=sweep_bits)
         self.loco.set_initial_condition(x0)
         self.lib, self.h = capi.lib(), self.loco._h
         capi.check(self.lib.mhpc_set_x0(self.h, capi.dptr(self.loco._x0)), "mhpc_set_x0")
@@ -466,6 +468,8 @@ def main():
                          "times, roofline); default = --steps")
     ap.add_argument("--ro-store", type=int, default=0,
                     help="line-search trials that store their records (0: default; tuning only)")
+    ap.add_argument("--sweep-bits", type=int, default=0,
+                    help="backward-sweep arithmetic: 0 / 64 double (default), 32 float (c5f32 only)")
     ap.add_argument("--sub-batches", type=int, default=0,
                     help="concurrently scheduled sub-batches per GPU, 1..4 (0 = automatic; tuning only)")
     ap.add_argument("--batch-sweep", default=None,
@@ -517,7 +521,8 @@ def main():
     if args.workload == "c2":
         return run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch)
     variants = (args.bws_variant, args.ro_variant, args.overlap, args.sub_batches, args.ro_store)
-    s = Solver(desc, opt, x0, local_rank, variants, layouts=layouts_of(args.workload, B, rank * B))
+    s = Solver(desc, opt, x0, local_rank, variants, layouts=layouts_of(args.workload, B, rank * B),
+               sweep_bits=args.sweep_bits)
     for _ in range(args.warmup):
         s.step()
 
@@ -625,6 +630,23 @@ def main():
                       "mixed_over_serial": (total / dt) / (B * args.steps / d5),
                       "note": "same problems, one homogeneous handle per layout, stepped in turn "
                               "(init + solve each), timed after the headline's timed region"}
+        # c5f32: the same step with the float backward sweep (MHPC_VARIANT_SWEEP_BITS = 32; the
+        # default fp32 sweep computes in double), timed after the headline
+        fsw = None
+        if world == 1 and args.workload == "c5f32" and args.sweep_bits == 0 and dist is None:
+            sf = Solver(desc, opt, x0, local_rank, variants, sweep_bits=32)
+            for _ in range(args.warmup):
+                sf.step()
+            torch.cuda.synchronize()
+            t6 = time.perf_counter()
+            for _ in range(args.steps):
+                sf.step()
+            torch.cuda.synchronize()
+            d6 = time.perf_counter() - t6
+            sf.close()
+            fsw = {"value": B * args.steps / d6, "unit": "solves/s", "ms_per_step": d6 / args.steps * 1e3,
+                   "note": "same step with the float backward sweep (sweep_bits 32), timed after the "
+                           "headline's timed region"}
         cpu, why = (None, "disabled" if world == 1 else "reported at N=1 only")
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or usable_cpus()
@@ -664,6 +686,10 @@ def main():
             line["north_star_b4096"] = ns
         if serial is not None:
             line["serial_homogeneous"] = serial
+        if fsw is not None:
+            line["float_sweep"] = fsw
+        if args.workload == "c5f32":
+            line["sweep_bits"] = args.sweep_bits or 64
         if shard is not None:
             line["sharding"] = shard
         print(json.dumps(line), file=_LINE_OUT or sys.stdout, flush=True)

@@ -317,6 +317,13 @@ void mhpc_destroy(mhpc_handle* h);
                                          an accepted trial without records is rolled out again
                                          into its slot (same arithmetic, bit for bit);
                                          0 = the default (4) */
+#define MHPC_VARIANT_SWEEP_BITS 5     /* which: arithmetic of the backward sweep: 64 (default,
+                                         also in an fp32 handle, whose sweep reads float records
+                                         and writes float gains but sums, factors and carries the
+                                         value function in double) or, fp32 handles only, 32
+                                         (the sweep in float, its 4x4 control block in double:
+                                         faster, 10-70x larger typical error vs the fp64 oracle,
+                                         DESIGN.md §5); 0 = default */
 int mhpc_set_kernel_variant(mhpc_handle* h, int which, int variant);
 
 /* ---- batched model evaluation on the device (kernel-level parity hooks) -----------

@@ -33,6 +33,7 @@ OVERLAP_VARIANTS = {"auto": 0, "on": 1, "off": 2}
 MHPC_VARIANT_SUBBATCH = 3
 MHPC_MAX_SUBBATCH = 4
 MHPC_VARIANT_RO_STORE = 4  # line-search trials storing their records (0 = default)
+MHPC_VARIANT_SWEEP_BITS = 5  # backward-sweep arithmetic: 64 double (default) / 32 float (fp32)
 MHPC_SOLVE_OK = 0
 MHPC_SOLVE_REG_ABORT = 1
 MHPC_SOLVE_NONFINITE = 2

@@ -48,6 +48,13 @@
 #include "mhpc_dpp.h"
 
 namespace MHPC_NS {
+int launch_problems(const SolveParams& sp);  // mhpc_kernels.hip
+// MHPC_BWS_VARIANT_NS: a second instantiation of this file in one library (the fp32 library's
+// float sweep, MHPC_BWS_F64=0) lives in a nested namespace -- its kernels and entry points
+// (launch_bws, bws_split, bws_auto_variant) do not collide with the default build's.
+#ifdef MHPC_BWS_VARIANT_NS
+namespace MHPC_BWS_VARIANT_NS {
+#endif
 
 // Arithmetic type of the whole-body knots' 4x4 control block (inverse, gains, and the H / G /
 // dV updates with them): the solve's type, or double in the fp32 build (MHPC_BWS_WIDE,
@@ -291,47 +298,54 @@ __device__ __forceinline__ void wave_lds_order() {
 }
 
 // Per-row LDS: the knot's Q rows for the Qxx transpose, and the value function at phase
-// boundaries.  Entry (r, c) of the 16 x 16 block lives at M[at(r, c)] = M[c * MP + r]: column-
-// major with an even pitch of 18 reals, and the RowLds of adjacent problems an odd number of
-// reals apart.  Then (tools/lds_banks.py, the banking table of MI355X_MICROARCH.md "LDS"):
-//  * a row write (lane rho stores (rho, j) for one j; 16-lane groups, 32 banks) touches 16
-//    consecutive words: conflict-free;
-//  * a transposed read (lane c loads (j, c) as one ds_read_b64, 32-lane groups over 64 banks):
-//    the 16 columns of one row sit on 16 distinct even word slots (18 c mod 32); the other half
-//    of the group reads row j + 7 (two-row layout: odd slots) or the next problem's block (odd
-//    offset): conflict-free.  fp32 (ds_read_b32, 32 banks): the same;
-//  * the diagonal's atomic add (rho, rho) at 19 rho: 16 distinct slots.
-// (Round 5: row-major, pitch 18 -- rows rho and rho + 8 on the same banks -- 34 % of the WB
-// sweep's LDS cycles were bank conflicts.)  The reads must stay single 8-byte reads: as
-// ds_read2_b64 / b128 pairs (what the compiler merges neighbouring reads into) the same
-// addresses conflict 2-way, so they go through lds_single.
-#ifndef MHPC_LDS_PITCH
-#define MHPC_LDS_PITCH 18
+// boundaries; entry (r, c) of the 16 x 16 block at M[at(r, c)].
+//
+// Default (round 5): row-major, pitch MP reals (16-byte aligned rows: the compiler writes a row
+// with ds_write_b128 and reads a transposed column as ds_read2_b64 pairs).  Rows rho and
+// rho + 8 share banks in the 8-lane groups of ds_write_b128, so 34 % of the WB sweep's LDS-array
+// cycles are bank conflicts (profiles/r05_sq_counters_b1024.txt).
+//
+// MHPC_LDS_COLMAJOR=1 (round 6): column-major with pitch 18 and the RowLds of adjacent problems
+// an odd number of reals apart; row writes (lane rho stores (rho, j); 16-lane groups over 32
+// banks) touch 16 consecutive words, and a transposed read issued as one ds_read_b64 per value
+// (32-lane groups over 64 banks: one row's 16 columns on 16 distinct even word slots, the
+// other half of the group on odd slots) is conflict-free -- the reads go through lds_single,
+// since the ds_read2_b64 pairs the compiler would merge them into conflict 2-way.  Measured
+// (profiles/r06_lds_layout_ab.txt): conflict cycles 34 % -> 0.8 % of the LDS-array cycles of
+// k_bws<2,2,2> and half the LDS-array cycles, all outputs bitwise equal -- but the WB half is
+// 1.2 % slower at batch 1024 and the one-row sweep 3.7 % slower in C5 at 4096: seven (fourteen)
+// single reads per knot instead of four (seven) paired ones cost more issue slots than the
+// conflicts cost LDS cycles in this latency-bound loop.  So it is not the default.
+#ifndef MHPC_LDS_COLMAJOR
+#define MHPC_LDS_COLMAJOR 0
 #endif
-// (experiment: pitch 17 with the reads left to the compiler's ds_read2_b64 pairs, whose 16-lane
-// halves are conflict-free for an odd pitch)
-#ifndef MHPC_LDS_SINGLE
-#define MHPC_LDS_SINGLE (MHPC_LDS_PITCH % 2 == 0)
-#endif
-constexpr int MP = MHPC_LDS_PITCH;
+#if MHPC_LDS_COLMAJOR
+constexpr int MP = 18;
 __device__ __forceinline__ constexpr int at(int r, int c) { return c * MP + r; }
-constexpr int kRowLdsPad = MP == 18 ? 1 : 3;  // 329 / 315 reals: adjacent problems' blocks on
-                                              // opposite bank halves
 struct RowLds {
   breal M[16 * MP];
   breal Gs[16];
   breal hx[14], Hs[9], h;
-  breal pad[kRowLdsPad];
+  breal pad;  // odd size (329 reals)
 };
-static_assert(sizeof(RowLds) % (2 * sizeof(breal)) == sizeof(breal), "RowLds must stay an odd number of reals");
+static_assert(sizeof(RowLds) == 329 * sizeof(breal), "RowLds must stay an odd number of reals");
+#else
+constexpr int MP = sizeof(breal) == 8 ? 18 : 20;
+__device__ __forceinline__ constexpr int at(int r, int c) { return r * MP + c; }
+struct RowLds {
+  alignas(16) breal M[16 * MP];
+  breal Gs[16];
+  breal hx[14], Hs[9], h;
+};
+#endif
 
 typedef __attribute__((address_space(3))) const breal lds_creal;
-// Read p[j] of an LDS array as one single-word read: the pointer passes through an empty asm
-// first (no instruction), so the compiler cannot merge it with the neighbouring reads into a
-// ds_read2 / b128 (whose lane groups differ, see RowLds).  The caller threads the returned
-// pointer into the next read, so no copy of the address register is needed.
+// Read q[j] of the LDS block.  Column-major layout: as one single-word read -- the pointer
+// passes through an empty asm first (no instruction), so the compiler cannot merge it with the
+// neighbouring reads into a ds_read2 / b128; the caller threads the pointer into the next read,
+// so no copy of the address register is needed.
 __device__ __forceinline__ breal lds_single(lds_creal*& q, int j) {
-  if (MHPC_LDS_SINGLE) asm volatile("" : "+v"(q));
+  if (MHPC_LDS_COLMAJOR) asm volatile("" : "+v"(q));
   return q[j];
 }
 struct BwsLds {
@@ -588,7 +602,7 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
     {
       lds_creal* tq = (lds_creal*)&rl.M[at(0, cr)];
 #pragma unroll
-      for (int j = 0; j < 14; ++j) T[j] = lds_single(tq, j);
+      for (int j = 0; j < 14; ++j) T[j] = lds_single(tq, at(j, 0));
     }
     wave_lds_order();
 
@@ -732,8 +746,10 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
   // column read in the transpose; lanes 14, 15 (no row of Qxx) read column 0 with lane 0 (a
   // broadcast): columns 14, 15 are never written in this layout, and a filler lane's H row
   // still enters 0 * x products, so it must stay finite
-  const int cr = xl ? rho : 0;
-  const int wo = rp ? 7 : 0;            // column of the row's first Q slot
+  // row-major layout: matrix column c at LDS column mcol(c) (row B's half 16-byte aligned)
+  auto mcol = [](int c) { return MHPC_LDS_COLMAJOR ? c : (c < 7 ? c : c + 1); };
+  const int cr = xl ? mcol(rho) : 0;
+  const int wo = rp ? mcol(7) : 0;      // LDS column of the row's first Q slot
   const int jr = rp ? 7 : 0;            // first matrix row of the row's H columns
   PendingKnot pend;
   pend.ok = false;
@@ -841,13 +857,13 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
     // ---- Qxx transpose: each row writes its half of the row rho ----
 #pragma unroll
     for (int s = 0; s < 7; ++s) rl.M[at(rho, wo + s)] = Q[s];
-    atomicAdd(&rl.M[at(rho, rho)], dg2);
+    atomicAdd(&rl.M[at(rho, xl ? mcol(rho) : rho)], dg2);
     wave_lds_order();
     breal T[7];
     {
       lds_creal* tq = (lds_creal*)&rl.M[at(jr, cr)];
 #pragma unroll
-      for (int s = 0; s < 7; ++s) T[s] = lds_single(tq, s);
+      for (int s = 0; s < 7; ++s) T[s] = lds_single(tq, at(s, 0));
     }
     wave_lds_order();
 
@@ -1127,7 +1143,7 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     {
       lds_creal* tq = (lds_creal*)&rl.M[at(0, cr)];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) T[j] = lds_single(tq, j);
+      for (int j = 0; j < 6; ++j) T[j] = lds_single(tq, at(j, 0));
     }
     wave_lds_order();
     BWS_SEG(10, sg2, sg3);
@@ -1541,7 +1557,6 @@ __global__ __launch_bounds__(64, PART == 1 ? MHPC_BWS_SRB_WAVES : 1) void k_bws(
 #ifndef MHPC_BWS_PAIRS_MAX_B
 #define MHPC_BWS_PAIRS_MAX_B 2048
 #endif
-int launch_problems(const SolveParams& sp);
 // Blocks of `rpw` problems over the layout groups (block_group)
 static unsigned bws_grid(const SolveParams& sp, int rpw) {
   long n = 0;
@@ -1583,6 +1598,9 @@ bool bws_split(const SolveParams& sp) {
   return sp.split_ok && sp.var_overlap != 2;
 }
 
+#ifdef MHPC_BWS_VARIANT_NS
+}  // namespace MHPC_BWS_VARIANT_NS
+#endif
 }  // namespace MHPC_NS
 
 #ifdef MHPC_BWS_TIMING

@@ -24,6 +24,11 @@ hipError_t launch_partials(const SolveParams&, const DevBufs&, hipStream_t, hipS
                            hipEvent_t);
 hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
 bool bws_split(const SolveParams&);
+#ifdef MHPC_FP32
+namespace fsweep {  // the float-arithmetic sweep (mhpc_bws.hip built with MHPC_BWS_F64=0)
+hipError_t launch_bws(const SolveParams&, const DevBufs&, real, int, hipStream_t);
+}
+#endif
 int ro_store_default();
 int ro_store_auto(const SolveParams&);
 hipError_t launch_cost(const SolveParams&, const DevBufs&, int, hipStream_t);
@@ -139,6 +144,7 @@ struct Handle {
   // problems, each block on its own stream pair; created on first use
   int nsub_req = 0;
   int ro_store_req = 0;  // MHPC_VARIANT_RO_STORE (0: by the batch's line-search shape)
+  int sweep_bits = 0;    // MHPC_VARIANT_SWEEP_BITS (0 = 64: the sweep computes in double)
   struct SubStreams {
     hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // s3: the partials' second group
     hipEvent_t fork = nullptr, join = nullptr, gate = nullptr, done = nullptr, pfork = nullptr,
@@ -785,6 +791,9 @@ static int issue_op(Handle* h, const SolveBlock& k, const SolveOp& op) {
   const DevBufs& d = k.d;
   const real ureg = h->opt.update_regularization;
   const bool split = bws_split(sp);
+#ifdef MHPC_FP32
+  auto launch_bws = h->sweep_bits == 32 ? fsweep::launch_bws : MHPC_NS::launch_bws;
+#endif
   switch (op.kind) {
     case OP_FULL:
       LAUNCH_ON(h, K_FULL, k.s1, launch_rollout(sp, d, op.al, 0, 0, 1, k.s1));
@@ -1402,6 +1411,12 @@ int api_set_kernel_variant(Handle* h, int which, int variant) {
     if (variant < 0 || variant > MAXC) return fail(MHPC_ERR_INVALID, "stored trials must be 0..32");
     h->ro_store_req = variant;
     sp.ro_store = variant ? variant : ro_store_auto(sp);
+    return MHPC_OK;
+  }
+  if (which == MHPC_VARIANT_SWEEP_BITS) {
+    if (variant != 0 && variant != 64 && !(variant == 32 && sizeof(real) == 4))
+      return fail(MHPC_ERR_INVALID, "sweep arithmetic must be 0 / 64 (double), or 32 (float) in an fp32 handle");
+    h->sweep_bits = variant;
     return MHPC_OK;
   }
   if (which == MHPC_VARIANT_SUBBATCH) {

@@ -518,13 +518,18 @@ class MHPCLocomotion:
         capi.check(capi.lib().mhpc_reset_kernel_stats(self._h), "mhpc_reset_kernel_stats")
 
     def set_kernel_variant(self, bws: str = "auto", rollout: str = "auto", overlap: str = "auto",
-                           sub_batches: int = 0, ro_store: int = 0):
+                           sub_batches: int = 0, ro_store: int = 0, sweep_bits: int = 0):
         """Pin the backward-sweep / line-search launch variant, the partials / sweep
         overlap, the number of concurrently scheduled sub-batches and the number of
         line-search trials that store their knot records (mhpc_set_kernel_variant); names in
         capi.BWS_VARIANTS / capi.RO_VARIANTS / capi.OVERLAP_VARIANTS, "auto" / 0 = chosen by
-        batch size and phase layout (ro_store 0: the default)."""
+        batch size and phase layout (ro_store 0: the default).  sweep_bits: arithmetic of the
+        backward sweep, 0 / 64 double (default), 32 float (fp32 handles only)."""
         L = capi.lib()
+        if sweep_bits or getattr(self, "_sweep_bits_pinned", False):
+            capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_SWEEP_BITS,
+                                                 int(sweep_bits)), "mhpc_set_kernel_variant")
+            self._sweep_bits_pinned = bool(sweep_bits)
         if ro_store or getattr(self, "_ro_store_pinned", False):
             capi.check(L.mhpc_set_kernel_variant(self._h, capi.MHPC_VARIANT_RO_STORE, int(ro_store)),
                        "mhpc_set_kernel_variant")

@@ -11,31 +11,63 @@ pytestmark = pytest.mark.gpu
 # Measured on MI355X (round 3): 64 problems -- traces identical 64/64, relative cost error
 # median 1.4e-5, max 1.8e-3; the batch-4103 sample of test_gpu_variants.py -- traces 63/63
 # (distinct indices), max 1.4e-3.  The fp32 build sums costs and compares the Armijo
-# condition in fp64 (mhpc_solver.h `acc`) and inverts the whole-body knots' 4x4 control block
-# in fp64 (mhpc_bws.hip, MHPC_BWS_WIDE): the gains of one fp32 sweep were 1e-2 off in the
-# stance phases (tools/diag_fp32_stages.py), the source of the earlier 5e-3..1e-2 cost errors;
-# fp64 cost accumulation alone left them unchanged.
+# condition in fp64 (mhpc_solver.h `acc`).  Round 6: its backward sweep computes in double by
+# default (mhpc_bws.hip MHPC_BWS_F64: float records in, float gains out) -- the float sweep's
+# rounding was the dominant error (tools/diag_fp32_stages.py: after one AL iteration the gains
+# agree to 2e-5 instead of 1e-2); the float sweep stays selectable per handle
+# (MHPC_VARIANT_SWEEP_BITS = 32) and keeps the round-5 bounds (test below).
 FP32_TRACE_MIN = 1.0      # problems that take the fp64 decisions (64-problem C5 case)
 FP32_TRACE_MIN_SAMPLE = 63 / 64  # the batch-4103 sample of test_gpu_variants.py: one fp32
                                  # decision may flip near its threshold (not two)
 FP32_J_TOL = 5e-3         # relative cost error of those problems, worst case
-FP32_J_MEDIAN_TOL = 5e-5  # ... and typical
+FP32_J_MEDIAN_TOL = 2e-5  # ... and typical (double sweep; float sweep 5e-5)
 # Trajectories, gains and value gradients of the same-trace problems against the fp64 oracle,
 # as norms relative to the oracle's per problem and phase-concatenated array:
-# e = ||a - b||_inf / max(1, ||b||_inf).  Stated target (round 5) for every array: the median
-# problem within 5e-3 and 95 % of the problems within 1e-2 (= the bulk of a batch accurate to
-# 1 %); a single ill-conditioned problem may reach 1e-1.  Why a distribution target: the error
-# of a problem is its conditioning times fp32's rounding -- the fp64 oracle's own answer moves
-# by up to 7.8e-5 (X) / 2.8e-4 (G) when only x0 is rounded to float (6e-8 relative), i.e. the
-# solve amplifies an input perturbation ~10^3-5x10^3 on its worst problems, and fp32
-# arithmetic perturbs every knot, not just x0 (tools/diag_fp32_x0.py: x0 rounding is not a
-# visible part of the fp32 error).  Measured (round 5, 64 problems): X median 2.2e-3 p95
-# 7.9e-3 max 1.9e-2; U 3.7e-4 / 2.2e-3 / 8.2e-3; K 3.4e-3 / 8.6e-3 / 1.1e-2; DU 4.8e-4 /
-# 1.1e-3 / 6.8e-3; G 1.3e-3 / 3.6e-3 / 6.2e-2 (one problem).
-FP32_ARRAY_MEDIAN = 5e-3
-FP32_ARRAY_P95 = 1e-2
+# e = ||a - b||_inf / max(1, ||b||_inf).
+# Double sweep (default), measured round 6 (64 problems; median / p95 / max): X 1.1e-4 /
+# 1.3e-3 / 2.3e-2, U 9.0e-5 / 1.4e-3 / 1.2e-2, K 4.9e-5 / 1.6e-3 / 1.7e-2, DU 2.7e-5 / 8.9e-4 /
+# 1.0e-2, G 4.8e-5 / 1.4e-3 / 9.5e-2 -- medians 20-70x and 95th percentiles 2-6x below the
+# float sweep's.  Every array's max is one problem, #50 of configs.x0_for(C5, 64): through the
+# first AL iteration it agrees with the oracle to 1e-5 like the rest, and in the second (ReB
+# barrier and a larger touchdown penalty active, 2-6 regularised sweep attempts) it leaves by
+# up to 1e-1 in G -- the fp32 rollouts' and Jacobians' rounding amplified ~1e6 there
+# (profiles/r06_fp32_worst_problem.txt).  Bounds: the distribution (median, 95th percentile),
+# every problem but that worst one within the round-4 per-array levels (X, G 2.5e-2; U, K, DU
+# 1e-2), and the worst within 1e-1.
+FP32_ARRAY_MEDIAN = 5e-4
+FP32_ARRAY_P95 = 5e-3
 FP32_ARRAY_MAX = 1e-1
+FP32_ARRAY_NEXT = {"X": 2.5e-2, "G": 2.5e-2, "U": 1e-2, "K": 1e-2, "DU": 1e-2}
 FP32_ARRAYS = ("X", "U", "K", "DU", "G")
+# float sweep (MHPC_VARIANT_SWEEP_BITS = 32), measured round 5/6: X 2.2e-3 / 7.9e-3 / 1.9e-2,
+# U 3.7e-4 / 2.2e-3 / 8.2e-3, K 3.4e-3 / 8.6e-3 / 1.1e-2, DU 4.8e-4 / 1.1e-3 / 6.8e-3,
+# G 1.3e-3 / 3.6e-3 / 6.2e-2 (problem 50)
+FP32F_ARRAY_MEDIAN = 5e-3
+FP32F_ARRAY_P95 = 1e-2
+
+
+def _solve_c5f32(B, sweep_bits=0):
+    from mhpc_minimal_env_amd import configs, locomotion as L
+    desc32 = configs.c5f32_desc()
+    x0 = configs.x0_for(desc32, B)
+    loco = L.MHPCLocomotion(desc=desc32, option=L.HSDDP_OPTION(), batch=B, device=0)
+    loco.set_kernel_variant(sweep_bits=sweep_bits)
+    loco.set_initial_condition(x0)
+    loco.initialization()
+    status = loco.solve_mhpc().copy()
+    sc = loco.get_scalars()
+    got = loco.concatenated()
+    loco.close()
+    return x0, status, sc, got
+
+
+def _array_errors(got, ref, same):
+    out = {}
+    for k in FP32_ARRAYS:
+        a = np.asarray(got[k], float)[same]
+        b = np.asarray(ref[k], float)[same]
+        out[k] = np.abs(a - b).max(axis=1) / np.maximum(1.0, np.abs(b).max(axis=1))
+    return out
 
 
 def test_c5_fp32_vs_fp64_oracle(need_gpu):
@@ -44,15 +76,7 @@ def test_c5_fp32_vs_fp64_oracle(need_gpu):
         pytest.skip("oracle not built")
     from mhpc_minimal_env_amd import configs, locomotion as L
     B = 64
-    desc32 = configs.c5f32_desc()
-    x0 = configs.x0_for(desc32, B)
-    loco = L.MHPCLocomotion(desc=desc32, option=L.HSDDP_OPTION(), batch=B, device=0)
-    loco.set_initial_condition(x0)
-    loco.initialization()
-    status = loco.solve_mhpc().copy()
-    sc = loco.get_scalars()
-    got = loco.concatenated()
-    loco.close()
+    x0, status, sc, got = _solve_c5f32(B)
     ref = O.solve(configs.c5_desc(64), L.HSDDP_OPTION().to_c(), x0, nthreads=8)
     assert np.isfinite(sc["J"]).all()
     same = (sc["trace"] == ref["trace"]).all(axis=1)
@@ -64,12 +88,65 @@ def test_c5_fp32_vs_fp64_oracle(need_gpu):
     assert rel[same].max() <= FP32_J_TOL
     assert np.median(rel[same]) <= FP32_J_MEDIAN_TOL
     # trajectories, gains and value gradients (verdict r3: not only J)
-    for k in FP32_ARRAYS:
-        a = np.asarray(got[k], float)[same]
-        b = np.asarray(ref[k], float)[same]
-        err = np.abs(a - b).max(axis=1) / np.maximum(1.0, np.abs(b).max(axis=1))
+    for k, err in _array_errors(got, ref, same).items():
         med, p95 = np.median(err), np.quantile(err, 0.95)
-        print(f"fp32 C5 {k}: rel err median {med:.2e} p95 {p95:.2e} max {err.max():.2e}")
+        srt = np.sort(err)
+        print(f"fp32 C5 {k}: rel err median {med:.2e} p95 {p95:.2e} max {srt[-1]:.2e} "
+              f"(problem {np.where(same)[0][err.argmax()]}), next {srt[-2]:.2e}")
         assert med <= FP32_ARRAY_MEDIAN, (k, med)
         assert p95 <= FP32_ARRAY_P95, (k, p95)
+        assert srt[-2] <= FP32_ARRAY_NEXT[k], (k, srt[-2])
+        assert srt[-1] <= FP32_ARRAY_MAX, (k, srt[-1])
+
+
+def test_c5_fp32_float_sweep_vs_fp64_oracle(need_gpu):
+    """The float sweep (MHPC_VARIANT_SWEEP_BITS = 32, the round-5 fp32 sweep): same decisions,
+    the round-5 distribution targets."""
+    import oracle as O
+    if not O.available():
+        pytest.skip("oracle not built")
+    from mhpc_minimal_env_amd import configs, locomotion as L
+    B = 64
+    x0, status, sc, got = _solve_c5f32(B, sweep_bits=32)
+    ref = O.solve(configs.c5_desc(64), L.HSDDP_OPTION().to_c(), x0, nthreads=8)
+    same = (sc["trace"] == ref["trace"]).all(axis=1)
+    rel = np.abs(sc["J"] - ref["J"]) / np.maximum(1.0, np.abs(ref["J"]))
+    assert same.mean() >= FP32_TRACE_MIN
+    assert rel[same].max() <= FP32_J_TOL
+    assert np.median(rel[same]) <= 5e-5
+    for k, err in _array_errors(got, ref, same).items():
+        med, p95 = np.median(err), np.quantile(err, 0.95)
+        print(f"fp32 C5 float sweep {k}: rel err median {med:.2e} p95 {p95:.2e} max {err.max():.2e}")
+        assert med <= FP32F_ARRAY_MEDIAN, (k, med)
+        assert p95 <= FP32F_ARRAY_P95, (k, p95)
         assert err.max() <= FP32_ARRAY_MAX, (k, err.max())
+
+
+def test_sweep_bits_variant_rules(need_gpu):
+    """32-bit sweep arithmetic exists for fp32 handles only; fp32 split / whole sweeps stay
+    bitwise equal in both arithmetics."""
+    from mhpc_minimal_env_amd import capi, configs, locomotion as L
+    lib = capi.lib()
+    loco = L.MHPCLocomotion(desc=configs.c3_desc(), option=L.HSDDP_OPTION(), batch=4, device=0)
+    try:
+        assert lib.mhpc_set_kernel_variant(loco._h, capi.MHPC_VARIANT_SWEEP_BITS, 32) == capi.MHPC_ERR_INVALID
+        assert lib.mhpc_set_kernel_variant(loco._h, capi.MHPC_VARIANT_SWEEP_BITS, 64) == capi.MHPC_OK
+        assert lib.mhpc_set_kernel_variant(loco._h, capi.MHPC_VARIANT_SWEEP_BITS, 16) == capi.MHPC_ERR_INVALID
+    finally:
+        loco.close()
+    desc32 = configs.c5f32_desc()
+    x0 = configs.x0_for(desc32, 12)
+    for bits in (64, 32):
+        outs = []
+        for overlap in ("on", "off"):
+            lo = L.MHPCLocomotion(desc=desc32, option=L.HSDDP_OPTION(), batch=12, device=0)
+            lo.set_kernel_variant(overlap=overlap, sweep_bits=bits)
+            lo.set_initial_condition(x0)
+            lo.initialization()
+            lo.solve_mhpc()
+            o = lo.concatenated()
+            o.update(lo.get_scalars())
+            lo.close()
+            outs.append(o)
+        for k in ("X", "U", "K", "DU", "G", "J", "V", "trace"):
+            np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=f"bits {bits} {k}")

@@ -1,7 +1,7 @@
 """Bitwise comparison of two builds of the library on the same solves (a kernel rewrite that
 must not change a single rounding).  Each build runs in its own process (MHPC_AMD_LIB):
 
-  python tools/lib_bitwise.py dump <out.npz> <workload> <batch> [bws variant] [precision]
+  python tools/lib_bitwise.py dump <out.npz> <workload> <batch> [bws variant] [precision] [sweep bits]
   python tools/lib_bitwise.py cmp <a.npz> <b.npz>
 
 Dump: C3 / C5 initial states of configs.x0_for, one full solve (every variant choice left
@@ -16,13 +16,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 KEYS = ("X", "U", "Y", "K", "DU", "G", "J", "dV_exp", "viol", "V", "dV", "trace", "status")
 
 
-def dump(out, workload, batch, bws="auto", precision=64):
+def dump(out, workload, batch, bws="auto", precision=64, sweep_bits=0):
     from mhpc_minimal_env_amd import configs, locomotion as L
     desc = configs.c5_desc(int(precision)) if workload == "c5" else configs.c3_desc()
     x0 = configs.x0_for(desc, batch)
     loco = L.MHPCLocomotion(desc=desc, option=L.HSDDP_OPTION(), batch=batch, device=0)
     try:
-        loco.set_kernel_variant(bws=bws)
+        if int(sweep_bits):
+            loco.set_kernel_variant(bws=bws, sweep_bits=int(sweep_bits))
+        else:
+            loco.set_kernel_variant(bws=bws)
         loco.set_initial_condition(x0)
         loco.initialization()
         status = loco.solve_mhpc().copy()
