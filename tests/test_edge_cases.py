@@ -40,3 +40,33 @@ def test_oracle_reproduces_edge_fixture(name):
         np.testing.assert_array_equal(r[k], g[k], err_msg=k)
     for k in ("J", "dV_exp", "viol", "V", "dV"):
         np.testing.assert_array_equal(r[k], g[k], err_msg=k)
+
+
+def test_overflow_case_conditioning():
+    """Why the overflow case is held to 1e-3 and not the solve tests' 1e-6
+    (tests/test_gpu_edge_cases.py): the oracle itself, given x0 perturbed by 1e-13 relative
+    (far below the device model's ~1e-11 difference to the reference's CasADi kernels),
+    takes the same decisions but moves its finite outputs by more than 1e-4 -- the surviving
+    violent trajectories amplify input rounding ~1e9..1e10, so no implementation that rounds
+    differently can meet 1e-6 there.  The armijo case, for contrast, moves by < 1e-7."""
+    if not O.available():
+        pytest.skip("oracle not built")
+
+    def spread(name, eps=1e-13):
+        desc, opt, x0 = E.inputs(name, batch=32)
+        ref = O.solve(desc, opt.to_c(), x0, nthreads=8)
+        rng = np.random.default_rng(1)
+        got = O.solve(desc, opt.to_c(), x0 * (1 + eps * rng.standard_normal(x0.shape)), nthreads=8)
+        assert (got["trace"] == ref["trace"]).all() and (got["status"] == ref["status"]).all()
+        e = 0.0
+        for k in ("X", "U", "K", "DU", "G"):
+            a, b = np.asarray(got[k], float), np.asarray(ref[k], float)
+            f = np.isfinite(a) & np.isfinite(b)
+            e = max(e, float(np.max(np.abs(a[f] - b[f]) / np.maximum(1.0, np.abs(b[f])))))
+        return e
+
+    e_over, e_armijo = spread("nonfinite"), spread("armijo_a")
+    print(f"oracle spread under a 1e-13 x0 perturbation: overflow case {e_over:.1e}, "
+          f"armijo case {e_armijo:.1e}")
+    assert e_over > 1e-4
+    assert e_armijo < 1e-7

@@ -35,7 +35,11 @@ def run_gpu(desc, opt, x0, **variant):
 # x0 perturbed 1000-fold: the finite problems' trajectories are violent enough to amplify
 # the ~1e-11 model difference to the CasADi kernels (tests/_util.py) to 2.3e-4 in DU, 7e-5 in
 # K, 4e-5 in U (costs <= 1.5e-7; measured on MI355X, the other cases stay <= 4e-9); every
-# decision, status and non-finite entry still matches
+# decision, status and non-finite entry still matches.  The bar cannot be 1e-6 here for any
+# implementation that rounds differently from the oracle: the oracle itself moves by 2.3e-3
+# (64 problems: 4.1e-3 in G) when its x0 is perturbed by 1e-13 relative
+# (tests/test_edge_cases.py::test_overflow_case_conditioning); the device is closer to it
+# than that.
 TOL = {"nonfinite": 1e-3}
 
 

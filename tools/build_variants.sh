@@ -18,6 +18,6 @@ while [ $# -ge 2 ]; do
   fi
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libmhpc_amd.so $d/bws.o $d/kern.o $C/_build/mhpc_runtime.o \
-      $k32 $b32 $C/_build/mhpc_runtime32.o $C/_build/mhpc_capi.o
+      $k32 $b32 $C/_build/mhpc_bws32f.o $C/_build/mhpc_runtime32.o $C/_build/mhpc_capi.o
   echo "$name: $flags" > $d/FLAGS
 done
