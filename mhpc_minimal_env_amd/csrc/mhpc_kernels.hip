@@ -1090,22 +1090,26 @@ hipError_t launch_store(const SolveParams& sp, const DevBufs& d, real* store, in
 // Jacobians of every WB knot of the nominal, by implicit differentiation of the contact KKT
 // system at the knot's solution (mhpc_model.h, WbKnot): the lane solves the knot's forward
 // dynamics once and then, per tangent direction, evaluates the inverse-dynamics residual in
-// dual numbers and solves with the knot's own factorisation.  Two launches over the knot
-// grid, a lane per (problem, WB knot) each: G = 0 the configuration directions 2..6 (plus
-// the knot's control / force cost derivatives), G = 1 the velocity directions 9..13 and the
-// controls 14..17; directions 0, 1, 7, 8 (base position / velocity) are exact zeros written
-// once at create.  k_partials_impact: the impact Jacobian Px at the end of the touchdown
+// dual numbers and solves with the knot's own factorisation.  One launch over the knot grid,
+// a lane per (problem, WB knot): the configuration directions 2..6, the velocity directions
+// 9..13, the controls 14..17 and the knot's control / force cost derivatives; directions 0, 1,
+// 7, 8 (base position / velocity) are exact zeros written once at create.  k_partials_impact: the impact Jacobian Px at the end of the touchdown
 // phases, one lane per (problem, impact, direction), dual numbers through wb_impact.
 // ============================================================================================
 // Direction groups, one launch each: [d0, d1) of the record's 18 columns (the controls'
-// columns need no residual, just a solve).  MHPC_PAR_GROUPS = 4 splits both groups in two
-// (more lanes, each with a shorter chain; the knot's forward dynamics is repeated per group).
+// columns need no residual, just a solve).  1 (default, round 6): every direction in one lane,
+// the knot's forward dynamics once.  2: G = 0 the configuration directions (+ the cost
+// derivatives), G = 1 the velocity and control directions, on two streams (rounds 3-5: more
+// lanes with shorter chains, the forward dynamics repeated per group); 4 splits both in two.
+// 1 vs 2, interleaved A/B (profiles/r06_partials_groups_ab.txt): C3 +0.6 % at 1024 (SRB half
+// beside them 0.186 -> 0.180 ms per launch), +1.1 % at 4096, C5 +1 %, mixed +0.5 %, C5 fp32
+// -0.2 %; bitwise equal.
 #ifndef MHPC_PAR_GROUPS
-#define MHPC_PAR_GROUPS 2
+#define MHPC_PAR_GROUPS 1
 #endif
 constexpr int kParGroups = MHPC_PAR_GROUPS;
 constexpr int kParD0[4] = {2, kParGroups == 4 ? 5 : 9, 9, 14};
-constexpr int kParD1[4] = {kParGroups == 4 ? 5 : 7, kParGroups == 4 ? 7 : 18, 14, 18};
+constexpr int kParD1[4] = {kParGroups == 1 ? 18 : kParGroups == 4 ? 5 : 7, kParGroups == 4 ? 7 : 18, 14, 18};
 
 // rec: the knot's piece of column block 0 (column c at rec + c * NK * 9, mhpc_solver.h par_col)
 template <int SF, int G>
@@ -1149,7 +1153,7 @@ __device__ __forceinline__ void partials_knot(const real* nk, real* rec, int NK)
 // than 256: at one wave per SIMD (the configuration group's 340 VGPRs) a block needs that many
 // SIMDs of one CU free at once, so smaller blocks fill the SIMDs the other group and the SRB
 // half of the sweep leave -- partials 1.10 -> 0.74 ms per step at batch 1024 (+1.9 % solves/s),
-// +0.3 % at 4096; 64 measured the same within noise
+// +0.3 % at 4096; 64 measured the same within noise (round 6, one group: again)
 #ifndef MHPC_PAR_BLOCK
 #define MHPC_PAR_BLOCK 128
 #endif
@@ -1818,15 +1822,15 @@ hipError_t launch_cost_grad(const SolveParams& sp, const DevBufs& d, int g, int 
                      b0, nb, lx, phix);
   return hipGetLastError();
 }
-// The direction groups write disjoint columns of the records: with a second stream s3 the
-// velocity / control group (G = 1, 252 VGPRs, two waves per SIMD) runs beside the
-// configuration group (340 VGPRs, one wave per SIMD) and fills the SIMDs its tail leaves;
-// the impact Jacobians (px: they read only the nominal) follow the shorter group on s3; s
-// joins s3 before returning.
+// With a second stream s3 the impact Jacobians (px: they read only the nominal) run there
+// beside the knot partials; with two direction groups (MHPC_PAR_GROUPS = 2, disjoint columns
+// of the records) the velocity / control group (G = 1, 252 VGPRs, two waves per SIMD) runs on
+// s3 too, beside the configuration group (340 VGPRs, one wave per SIMD), and the impact
+// Jacobians follow it; s joins s3 before returning.
 hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t s, hipStream_t s3,
                            hipEvent_t fork, hipEvent_t join) {
   const unsigned tk = grid_items(sp, sp.gpk, 0, MHPC_PAR_BLOCK), ti = grid_items(sp, sp.gpi, 0, 256);
-  const bool two = s3 && fork && join && kParGroups == 2 && tk > 0;
+  const bool two = s3 && fork && join && kParGroups <= 2 && tk > 0;
   if (two) {
     hipError_t e = hipEventRecord(fork, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(s3, fork, 0);
@@ -1839,7 +1843,7 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   if (tk > 0) {
     constexpr int nt = MHPC_PAR_BLOCK;
     const dim3 grid(tk);
-    hipLaunchKernelGGL(k_partials<1>, grid, dim3(nt), 0, two ? s3 : s, sp, d);
+    if (kParGroups > 1) hipLaunchKernelGGL(k_partials<1>, grid, dim3(nt), 0, two ? s3 : s, sp, d);
     hipLaunchKernelGGL(k_partials<0>, grid, dim3(nt), 0, s, sp, d);
     if (kParGroups == 4) {
       hipLaunchKernelGGL(k_partials<2>, grid, dim3(nt), 0, s, sp, d);
