@@ -1145,7 +1145,8 @@ __device__ __forceinline__ void partials_knot(const real* nk, real* rec, int NK)
   }
 }
 
-// MHPC_PAR_MINB: blocks per CU the register allocator must allow for the partials (1: no cap)
+// MHPC_PAR_MINB: blocks per CU the register allocator must allow for the partials (1: no cap;
+// round 6: 2 in the fp32 build, 258 -> 256 VGPRs, two waves per SIMD, measured identical)
 #ifndef MHPC_PAR_MINB
 #define MHPC_PAR_MINB 1
 #endif
@@ -1843,9 +1844,9 @@ hipError_t launch_partials(const SolveParams& sp, const DevBufs& d, hipStream_t 
   if (tk > 0) {
     constexpr int nt = MHPC_PAR_BLOCK;
     const dim3 grid(tk);
-    if (kParGroups > 1) hipLaunchKernelGGL(k_partials<1>, grid, dim3(nt), 0, two ? s3 : s, sp, d);
+    if constexpr (kParGroups > 1) hipLaunchKernelGGL(k_partials<1>, grid, dim3(nt), 0, two ? s3 : s, sp, d);
     hipLaunchKernelGGL(k_partials<0>, grid, dim3(nt), 0, s, sp, d);
-    if (kParGroups == 4) {
+    if constexpr (kParGroups == 4) {
       hipLaunchKernelGGL(k_partials<2>, grid, dim3(nt), 0, s, sp, d);
       hipLaunchKernelGGL(k_partials<3>, grid, dim3(nt), 0, s, sp, d);
     }
