@@ -22,10 +22,12 @@ def load(path, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            m = re.search(r"mhpc\d*::(\w+)", name)
-            key = m.group(1) if m else name
+            m = re.search(r"mhpc\d*::(fsweep::)?(\w+)", name)
+            key = m.group(2) if m else name
             if key == "k_bws" and re.search(r"k_bws<\d+, 1, \d+>", name):
                 key = "k_bws_srb"  # SRB half of the split backward sweep (k_bws<RPW, PART 1, RPP>)
+            if m and m.group(1):  # the fp32 library's float sweep (bench.py c5f32 float_sweep leg)
+                key = "fsweep." + key
             if key == "k_rollout":  # one launch group: the line search + the re-roll kernel
                 v = re.search(r"k_rollout<(\w+), (\w+), (\w+)>", name)
                 key = "k_rollout." + ("".join(x[0] for x in v.groups()) if v else "x")
