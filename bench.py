@@ -376,6 +376,16 @@ def run_c2(args, desc, opt, x0, B, rank, world, local_rank, dist, torch):
         dist.destroy_process_group()
 
 
+def knot_steps_per_rollout(wl, desc) -> int:
+    """Rollout knots of one problem for SURVEY.md 8(d)'s "knot-steps/s" diagnostic (the serial
+    knot-steps of the reference's solve: every knot swept backward, failed attempts included,
+    plus one rollout's knots per forward sweep and per line search, whose trials run side by
+    side: one rollout deep).  0 for the mixed workload, whose batch counters do not separate
+    its layouts, and for C2."""
+    if wl not in ("c3", "c5", "c5f32"):
+        return 0
+    return sum(desc.N[p] - 1 for p in range(desc.n_phases))
+
 def run_sweep(args, torch):
     """One JSON line per batch size (1 GPU): throughput and the latency of one controller
     solve (init + solve of the batch; at batch 1 the real-time MPC tick of
@@ -389,7 +399,8 @@ def run_sweep(args, torch):
         for _ in range(args.warmup):
             s.step()
         solve_ms = 0.0
-        ddp = 0
+        ddp = knots = 0
+        kroll = knot_steps_per_rollout(args.workload, desc)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -397,6 +408,7 @@ def run_sweep(args, torch):
             c = s.loco.get_counters()
             solve_ms += c["solve_ms"]
             ddp += c["ddp_iters"]
+            knots += c["bws_knots"] + (c["fwd_sweeps"] + c["ddp_iters"]) * kroll
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         # per-kernel event timing in separate steps (see main)
@@ -414,7 +426,8 @@ def run_sweep(args, torch):
             "latency_ms_per_solve_call": dt / args.steps * 1e3,
             "solve_only_ms": solve_ms / args.steps,
             "solve_only_per_s": B * args.steps / (solve_ms / 1e3) if solve_ms > 0 else None,
-            "ddp_iters_per_s": ddp / dt, "steps": args.steps, "warmup": args.warmup,
+            "ddp_iters_per_s": ddp / dt, "knot_steps_per_s": knots / dt if kroll else None,
+            "steps": args.steps, "warmup": args.warmup,
             "dtype": "f32" if args.workload == "c5f32" else "f64",
             "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
             "profiled_steps": prof_steps,
@@ -533,6 +546,8 @@ def main():
 
     solve_ms = 0.0
     ddp_iters = 0
+    knot_steps = 0
+    kroll = knot_steps_per_rollout(args.workload, desc)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -540,6 +555,7 @@ def main():
         c = s.loco.get_counters()
         solve_ms += c["solve_ms"]
         ddp_iters += c["ddp_iters"]
+        knot_steps += c["bws_knots"] + (c["fwd_sweeps"] + c["ddp_iters"]) * kroll
     barrier()
     dt = time.perf_counter() - t0
     # per-kernel HIP-event timing (an event pair around every launch) in separate steps after
@@ -553,21 +569,22 @@ def main():
     s.loco.set_profiling(False)
 
     stats = s.loco.kernel_stats()
-    tens = torch.tensor([dt, solve_ms / 1e3, float(ddp_iters)], dtype=torch.float64, device=tdev)
+    tens = torch.tensor([dt, solve_ms / 1e3, float(ddp_iters), float(knot_steps)],
+                        dtype=torch.float64, device=tdev)
     shard = None
     if dist is not None:
         tmax = tens[:2].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = tens[2:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dt, solve_s, ddp_total = float(tmax[0]), float(tmax[1]), float(tsum[0])
+        dt, solve_s, ddp_total, knot_total = float(tmax[0]), float(tmax[1]), float(tsum[0]), float(tsum[1])
         # per-problem summaries of every rank (RCCL all-gather; outside the timed region)
         allp = sharding.gather_summaries(s.summary(rank * B),
                                          device=tdev if args.backend == "nccl" else None)
         shard = {"ranks": dist.get_world_size(), "backend": dist.get_backend(),
                  "gathered_problems": int(len(allp))}
     else:
-        solve_s, ddp_total = solve_ms / 1e3, float(ddp_iters)
+        solve_s, ddp_total, knot_total = solve_ms / 1e3, float(ddp_iters), float(knot_steps)
     s.close()
 
     if rank == 0:
@@ -676,6 +693,7 @@ def main():
                 "parallelism": f"batch-sharded x{world}",
             },
             "ddp_iters_per_s": ddp_total / dt,
+            "knot_steps_per_s": knot_total / dt if kroll else None,
             "solve_only_per_s": total / solve_s if solve_s > 0 else None,
             "kernel_ms_per_step": {k: v["ms"] / max(prof_steps, 1) for k, v in stats.items()},
             "profiled_steps": prof_steps,

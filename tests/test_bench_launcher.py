@@ -49,3 +49,14 @@ def test_world_size_must_match_gpus():
 def test_usable_cpus_is_positive(bench):
     n = bench.usable_cpus()
     assert 1 <= n <= (os.cpu_count() or n)
+
+
+def test_knot_steps_per_rollout(bench):
+    """SURVEY.md 8(d)'s knot-steps diagnostic: C3 rolls 4 x 79 knots per rollout, C5 (N = 80,
+    100 alternating over 10 phases) 5 x 79 + 5 x 99; the mixed workload reports none."""
+    from mhpc_minimal_env_amd import configs
+    assert bench.knot_steps_per_rollout("c3", configs.c3_desc()) == 316
+    d5 = configs.c5_desc()
+    assert bench.knot_steps_per_rollout("c5", d5) == sum(d5.N[p] - 1 for p in range(10))
+    assert bench.knot_steps_per_rollout("c5", d5) == 5 * 79 + 5 * 99
+    assert bench.knot_steps_per_rollout("mixed", configs.c3_desc()) == 0
