@@ -216,10 +216,14 @@ def roofline_of(stats: dict, batch: int, wl: str = "c3") -> dict:
     r["per_kernel"] = per
     if flops_per_launch > 0 and per_launch_s > 0:
         tf = flops_per_launch / per_launch_s / 1e12
+        model = ("per trial knot: the reference's dynamics in CasADi generated-code operation "
+                 "counts (Dyn_BS/FS 2301, Dyn_FL 1441, FBDynamics 44) + feedback + Euler step"
+                 if dom.startswith("k_rollout") else
+                 "reference dense formulation (compute_Qfunction + valuefunction_update per "
+                 "knot, impact-aware step)")
         r["valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tf / FP64_PEAK_TFS, "alg_flops_per_launch": flops_per_launch,
-                     "flop_model": "reference dense formulation (compute_Qfunction + "
-                                   "valuefunction_update per knot, impact-aware step)"}
+                     "flop_model": model}
     return r
 
 

@@ -92,6 +92,7 @@ struct ProbLayout {
 // Algorithmic bytes per problem of one layout
 struct ByteModel {
   double roll_read = 0, roll_write = 0, roll_term = 0, par = 0, init = 0, cost = 0;
+  double roll_flops = 0;  // one trial rollout (the line search's flop model)
 };
 
 struct Handle {
@@ -189,6 +190,16 @@ static void build_layout(Layout& L, const mhpc_problem_desc& desc, int rot_wb, i
 // Algorithmic HBM bytes (fp64) of one problem for each kernel's unit of work.
 constexpr double kB = sizeof(real);  // bytes per element of the solve's arithmetic type
 
+// Line-search flop model per trial knot (SURVEY.md 8d secondary roofline): the reference's
+// dynamics in CasADi's generated-code assignment counts (Dyn_BS / Dyn_FS 2301,
+// Dyn_FL 1441, FBDynamics 44 -- scalar operations incl. loads, so an upper estimate), plus the
+// feedback u = u_nom + eps du + K (x - x_nom) and the Euler step (WB: 14 + 4 * 28 + 8 + 28;
+// SRB: 6 + 4 * 12 + 8 + 12).  The running costs (the second wave) are not counted.
+static double ro_knot_flops(int mode, bool wb) {
+  if (!wb) return 44 + 74;
+  return (mode == 1 || mode == 3 ? 2301.0 : 1441.0) + 162;
+}
+
 static ByteModel byte_model(const Layout& L) {
   ByteModel m;
   double rr = 14 * 8, rw = 0, rt = 0, pb = 0, ib = L.NK * kB, cb = 0;
@@ -201,6 +212,7 @@ static ByteModel byte_model(const Layout& L) {
     // a storing candidate writes x,u,y of every knot, every candidate x at the last knot
     rw += (N - 1) * kB * (n + 8);
     rt += n * kB;
+    m.roll_flops += (N - 1) * ro_knot_flops(L.mode[p], wb);
     // k_cost: nominal x,u(,y) of every knot + refpos
     cb += (N - 1) * kB * (n + 4 + (wb ? 4 : 0) + 1) + kB * (n + 1);
     // k_init: x,u,y written for every knot (WB and SRB)
@@ -984,6 +996,7 @@ int api_solve(Handle* h, int32_t* status) {
     h->kbytes[K_LS] += cg[C_LS_LAUNCH] * m.roll_read +
                        cg[C_LS_RUN] * (m.roll_write * stored / sp.n_cand + m.roll_term);
     h->kbytes[K_PAR] += cg[C_PAR_RUN] * m.par;
+    h->kflops[K_LS] += cg[C_LS_RUN] * m.roll_flops;
   }
   // the SRB half of a split sweep: the SRB knots of every first attempt; the rest (WB knots,
   // impact steps, SRB knots of retries) is the WB half's / the whole sweep's
