@@ -441,7 +441,9 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
   // second control column set (lanes 14, 15), one cost derivative per lane (broadcast below)
   constexpr int NR = STANCE ? 9 : 7;  // rows of a record column read
   constexpr int NCS = STANCE ? 14 : 8;  // cost derivatives (lu, luu [, ly, lyy])
-  breal pr1[NR], pr2[NR], pcv, pxn, ppos;
+  // (in the record type: a float record converted at load time would make the compiler wait
+  // for the load there, a knot early; converted at the use instead -- the same values)
+  real pr1[NR], pr2[NR], pcv, pxn, ppos;
   const int c1 = rho;            // record column of W1 (0..15)
   const int c2 = 16 + (t & 1);   // second set: control columns 2, 3 (lanes 14, 15)
   const int cq = t < NCS ? t : 0;
@@ -501,29 +503,30 @@ __device__ int sweep_wb(const SolveParams& sp, const DevBufs& d, const Layout& L
     // ---- the knot's derivatives (prefetched) ----
     breal W1[7], W2[7], G2o[2], G22[2];
 #pragma unroll
-    for (int r = 0; r < 7; ++r) W1[r] = __builtin_fma(pr1[r], dt, base[r]);
+    for (int r = 0; r < 7; ++r) W1[r] = __builtin_fma(breal(pr1[r]), dt, base[r]);
 #pragma unroll
-    for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(pr2[r], dt, breal(0.0));
+    for (int r = 0; r < 7; ++r) W2[r] = __builtin_fma(breal(pr2[r]), dt, breal(0.0));
     // C, D rows: copied out of the prefetch registers (a fresh value each, so the prefetch
     // buffer is dead before it is reloaded; a buffer live across its own reload costs a copy
     // at the back edge that waits for every outstanding memory operation, stores included)
     G2o[0] = G2o[1] = G22[0] = G22[1] = breal(0.0);
     if (STANCE) {
-      asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
-      asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
-      asm volatile("" : "=v"(G22[0]) : "0"(pr2[NR - 2]));
-      asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
+      asm volatile("" : "=v"(G2o[0]) : "0"(breal(pr1[NR - 2])));
+      asm volatile("" : "=v"(G2o[1]) : "0"(breal(pr1[NR - 1])));
+      asm volatile("" : "=v"(G22[0]) : "0"(breal(pr2[NR - 2])));
+      asm volatile("" : "=v"(G22[1]) : "0"(breal(pr2[NR - 1])));
     }
     // cost derivatives: lane q of the row holds entry q of (lu, luu, ly, lyy)
     breal luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
-    const breal lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
-    luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
+    const breal pcvd = pcv;
+    const breal lu0 = rbc<0>(pcvd), lu1 = rbc<1>(pcvd), lu2 = rbc<2>(pcvd), lu3 = rbc<3>(pcvd);
+    luu[0] = rbc<4>(pcvd); luu[1] = rbc<5>(pcvd); luu[2] = rbc<6>(pcvd); luu[3] = rbc<7>(pcvd);
     if (STANCE) {
-      ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
-      lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
+      ly[0] = rbc<8>(pcvd); ly[1] = rbc<9>(pcvd);
+      lyy[0] = rbc<10>(pcvd); lyy[1] = rbc<11>(pcvd); lyy[2] = rbc<12>(pcvd); lyy[3] = rbc<13>(pcvd);
     }
-    const breal rxi = rho == 0 ? ppos : rxc;
-    const breal lx = w2 * (pxn - rxi);
+    const breal rxi = rho == 0 ? breal(ppos) : rxc;
+    const breal lx = w2 * (breal(pxn) - rxi);
     const breal lu01 = (t & 1) ? lu1 : lu0;
     const breal l1 = xl ? lx : lu01;
     const breal l2 = (t & 1) ? lu3 : lu2;
@@ -713,7 +716,7 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
   const real* pos = d.refpos + (size_t)b * sp.NK + ko;
   constexpr int NR = STANCE ? 9 : 7;
   constexpr int NCS = STANCE ? 14 : 8;
-  breal pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;
+  real pr1[NR], prb[NR], pr2[NR], pcv, pxn, ppos;  // record type, see sweep_wb
   const int c2 = 16 + (t & 1);
   const int cq = t < NCS ? t : 0;
   // the phase's operand / output bases (knot 0): a knot adds k times its record stride
@@ -777,28 +780,29 @@ __device__ int sweep_wb2(const SolveParams& sp, const DevBufs& d, const Layout& 
     breal Wo[7], Wb[7], W2[7], G2o[2], G2b[2], G22[2];
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
-      Wo[r] = __builtin_fma(pr1[r], dt, base[r]);
-      Wb[r] = __builtin_fma(prb[r], dt, baseb[r]);
-      W2[r] = __builtin_fma(pr2[r], dt, breal(0.0));
+      Wo[r] = __builtin_fma(breal(pr1[r]), dt, base[r]);
+      Wb[r] = __builtin_fma(breal(prb[r]), dt, baseb[r]);
+      W2[r] = __builtin_fma(breal(pr2[r]), dt, breal(0.0));
     }
     G2o[0] = G2o[1] = G2b[0] = G2b[1] = G22[0] = G22[1] = breal(0.0);
     if (STANCE) {  // fresh values (see sweep_wb)
-      asm volatile("" : "=v"(G2o[0]) : "0"(pr1[NR - 2]));
-      asm volatile("" : "=v"(G2o[1]) : "0"(pr1[NR - 1]));
-      asm volatile("" : "=v"(G2b[0]) : "0"(prb[NR - 2]));
-      asm volatile("" : "=v"(G2b[1]) : "0"(prb[NR - 1]));
-      asm volatile("" : "=v"(G22[0]) : "0"(pr2[NR - 2]));
-      asm volatile("" : "=v"(G22[1]) : "0"(pr2[NR - 1]));
+      asm volatile("" : "=v"(G2o[0]) : "0"(breal(pr1[NR - 2])));
+      asm volatile("" : "=v"(G2o[1]) : "0"(breal(pr1[NR - 1])));
+      asm volatile("" : "=v"(G2b[0]) : "0"(breal(prb[NR - 2])));
+      asm volatile("" : "=v"(G2b[1]) : "0"(breal(prb[NR - 1])));
+      asm volatile("" : "=v"(G22[0]) : "0"(breal(pr2[NR - 2])));
+      asm volatile("" : "=v"(G22[1]) : "0"(breal(pr2[NR - 1])));
     }
     breal luu[4], ly[2] = {0, 0}, lyy[4] = {0, 0, 0, 0};
-    const breal lu0 = rbc<0>(pcv), lu1 = rbc<1>(pcv), lu2 = rbc<2>(pcv), lu3 = rbc<3>(pcv);
-    luu[0] = rbc<4>(pcv); luu[1] = rbc<5>(pcv); luu[2] = rbc<6>(pcv); luu[3] = rbc<7>(pcv);
+    const breal pcvd = pcv;
+    const breal lu0 = rbc<0>(pcvd), lu1 = rbc<1>(pcvd), lu2 = rbc<2>(pcvd), lu3 = rbc<3>(pcvd);
+    luu[0] = rbc<4>(pcvd); luu[1] = rbc<5>(pcvd); luu[2] = rbc<6>(pcvd); luu[3] = rbc<7>(pcvd);
     if (STANCE) {
-      ly[0] = rbc<8>(pcv); ly[1] = rbc<9>(pcv);
-      lyy[0] = rbc<10>(pcv); lyy[1] = rbc<11>(pcv); lyy[2] = rbc<12>(pcv); lyy[3] = rbc<13>(pcv);
+      ly[0] = rbc<8>(pcvd); ly[1] = rbc<9>(pcvd);
+      lyy[0] = rbc<10>(pcvd); lyy[1] = rbc<11>(pcvd); lyy[2] = rbc<12>(pcvd); lyy[3] = rbc<13>(pcvd);
     }
-    const breal rxi = rho == 0 ? ppos : rxc;
-    const breal lx = w2 * (pxn - rxi);
+    const breal rxi = rho == 0 ? breal(ppos) : rxc;
+    const breal lx = w2 * (breal(pxn) - rxi);
     const breal lu01 = (t & 1) ? lu1 : lu0;
     const breal l1 = xl ? lx : lu01;
     const breal l2 = (t & 1) ? lu3 : lu2;
@@ -1041,7 +1045,7 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
   // a lane's knot operands from the nominal: its two W-row-5 operands (or x, z, u), its own
   // entry, the position reference
   struct Ops {
-    breal e0, e1, v, pos, xs[2], us[4];
+    real e0, e1, v, pos, xs[2], us[4];  // record type, see sweep_wb
   };
   const real* tk0 = traj_ptr(sp, d, b, rc.nom, ko);  // knot k adds k KS
   const int oe0 = srb_w2_off(cj, 0), oe1 = srb_w2_off(cj, 1);
@@ -1100,10 +1104,14 @@ __device__ int sweep_srb(const SolveParams& sp, const DevBufs& d, const Layout& 
     breal W[3];
     W[0] = W0c;
     W[1] = W1c;
-    W[2] = LANE_OPS ? srb_w2_lane(cj, o.e0, o.e1, foot, cs, dt)
-                    : srb_w_entry(2, cj, o.xs, o.us, foot, cs, dt);
-    const breal rxi = rho == 0 ? o.pos : rxc;
-    const breal l1 = w2 * (o.v - rxi);
+    if (LANE_OPS) {
+      W[2] = srb_w2_lane(cj, breal(o.e0), breal(o.e1), foot, cs, dt);
+    } else {
+      const breal xs[2] = {o.xs[0], o.xs[1]}, us[4] = {o.us[0], o.us[1], o.us[2], o.us[3]};
+      W[2] = srb_w_entry(2, cj, xs, us, foot, cs, dt);
+    }
+    const breal rxi = rho == 0 ? breal(o.pos) : rxc;
+    const breal l1 = w2 * (breal(o.v) - rxi);
     const bool gate = go(rc);
     rc.kn += gate ? 1 : 0;
     asm volatile("" ::"v"(W[2]), "v"(l1));  // see sweep_wb
